@@ -1,0 +1,196 @@
+/*
+ * ydbl.h — C ABI of libydbl.so, the MI355X (gfx950) kernels behind the
+ * YOLO-DBL inference hot path (backbone/neck conv stack, Detect decode,
+ * class-wise NMS).
+ *
+ * Boundary rules:
+ *   - every entry point is stateless and reentrant, takes caller-owned DEVICE
+ *     pointers plus an explicit hipStream_t (passed as void*), and only
+ *     enqueues work on that stream (graph-capturable: no malloc, no sync);
+ *   - the return value is 0 on success, otherwise a YDBL_E* code, and
+ *     ydbl_last_error() returns a thread-local message (the Python layer
+ *     raises RuntimeError with it, mirroring the reference's exceptions /
+ *     asserts, e.g. U/utils/ops.py:217-218, U/data/loaders.py:554-560);
+ *   - activations are NHWC.  A "view" is (pointer, N, H, W, C, channel
+ *     stride cs): element (n,y,x,c) lives at ptr[((n*H+y)*W+x)*cs + c].
+ *     Writing into a channel slice of a wider buffer (cs > C) is how Concat,
+ *     chunk() and C2f/C3 concatenations are done without copies.
+ *
+ * Reference interfaces replaced (paths relative to
+ * /root/reference/models/YOLO/ultralytics):
+ *   ydbl_conv2d_nhwc       <- nn/modules/conv.py:39-63 Conv.forward_fuse (conv+bias+SiLU after
+ *                             nn/tasks.py:207-235 fuse), conv.py:91-108 DSConv pointwise+BN+SiLU,
+ *                             nn.Conv2d 1x1 in Detect/LSKblock/DySample, nn.Linear in AdaHG
+ *   ydbl_dwconv2d_nhwc     <- depthwise nn.Conv2d (DSConv.dw conv.py:98, DWConv conv.py:128-133,
+ *                             GhostConv.cv2 conv.py:194, LSKblock.conv0/conv_spatial LSKA.py:31-32)
+ *   ydbl_input_nchw_to_nhwc<- BasePredictor.preprocess engine/predictor.py:116-134 (+ LoadTensor /255)
+ *   ydbl_gate_add          <- FullPAD_Tunnel.forward nn/modules/block.py:1954-1956
+ *   ydbl_pool_up_concat    <- FuseModule.forward block.py:1831-1840, DownsampleConv block.py:1927
+ *   ydbl_dysample          <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
+ *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
+ *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708
+ *   ydbl_detect_decode     <- Detect._inference head.py:143-181 + DFL block.py:79-83 +
+ *                             make_anchors/dist2bbox utils/tal.py:333-357 + NMS candidate
+ *                             filter utils/ops.py:234-276
+ *   ydbl_pred_candidates   <- utils/ops.py:234-276 on a [B,4+nc,A] prediction tensor
+ *   ydbl_nms               <- utils/ops.py:278-310 (+ torchvision.ops.nms, torchvision 0.23.0),
+ *                             with clip_boxes utils/ops.py:319-338 as reached through
+ *                             scale_boxes :92-127 for tensor sources (gain 1, pad 0)
+ */
+#ifndef YDBL_H
+#define YDBL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { YDBL_OK = 0, YDBL_EINVAL = 1, YDBL_ELAUNCH = 2, YDBL_ECAPACITY = 3 };
+enum { YDBL_F32 = 0, YDBL_F16 = 1 };
+enum { YDBL_ACT_NONE = 0, YDBL_ACT_SILU = 1, YDBL_ACT_GELU = 2, YDBL_ACT_SIGMOID = 3 };
+enum { YDBL_RES_NONE = 0, YDBL_RES_ADD = 1, YDBL_RES_MUL = 2 };
+
+typedef struct {
+  void* ptr;  /* device pointer to element (0,0,0,0) of the view */
+  int32_t n, h, w, c;
+  int32_t cs; /* channel stride in elements (>= c) */
+  int32_t dtype;
+} ydbl_view;
+
+/* Dense (groups = 1) convolution, implicit GEMM on MFMA (f16: 16x16x32, f32: exact 16x16x4).
+ * y = act(conv(x, w) + bias); then res_mode ADD: y = r + y, MUL: y = r * y.
+ * w: [cout][kh][kw][cin] in the view dtype, with cin == x.c (x.c must be a multiple of 8),
+ *    rows padded to kpad = round_up(kh*kw*cin, 32) elements with zeros.
+ * bias: fp32 [cout] or NULL.  r: view or NULL.
+ * x.c, y.c multiples of 8 except y.c may be < 8 only when y.cs is a multiple of 4. */
+typedef struct {
+  ydbl_view x, y, r;
+  const void* w;
+  const float* bias;
+  int32_t kh, kw, stride, pad, dil;
+  int32_t kpad;
+  int32_t act, res_mode;
+} ydbl_conv_desc;
+int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream);
+
+/* Depthwise convolution (groups = C), fp32 arithmetic.
+ * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).
+ * w: fp32 [kh][kw][c]; bias: fp32 [c] or NULL; r: view or ignored. */
+typedef struct {
+  ydbl_view x, y, r;
+  const float* w;
+  const float* bias;
+  int32_t kh, kw, stride, pad, dil;
+  int32_t act, res_mode;
+} ydbl_dwconv_desc;
+int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream);
+
+/* NCHW fp32 image batch -> NHWC view (channels >= 3 zero-filled up to y.cs), optional scale (1/255). */
+int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,
+                            const ydbl_view* y, void* stream);
+
+/* y = a + gate * b (FullPAD_Tunnel). */
+int ydbl_gate_add(const ydbl_view* a, const ydbl_view* b, float gate, const ydbl_view* y, void* stream);
+
+/* y[..., off0:] = avgpool2(p_lo); y[..., off1:] = p_mid; y[..., off2:] = nearest_up2(p_hi).
+ * Any of p_lo / p_mid / p_hi may be NULL (DownsampleConv uses p_lo only). */
+int ydbl_pool_up_concat(const ydbl_view* p_lo, const ydbl_view* p_mid, const ydbl_view* p_hi,
+                        const ydbl_view* y, void* stream);
+
+/* DySample 'lp' x2 sampling: off fp32 view [n,h,w,8*groups] holding 0.25*offset+init_pos
+ * (channel k = coord*4g + group*4 + i*2 + j), bilinear border grid_sample of x into y [n,2h,2w,c]. */
+int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y, void* stream);
+
+/* LSKblock gate: attn view = [a1 | a2] (2*half channels, each half = dim/2);
+ * agg = [mean_c, max_c](attn); sig = sigmoid(conv7x7(agg) + sb); out = a1*sig0 + a2*sig1.
+ * sw: fp32 [2][2][7][7] (torch layout), sb: fp32 [2]. */
+int ydbl_lsk_gate(const ydbl_view* attn, const float* sw, const float* sb, const ydbl_view* out,
+                  void* workspace, void* stream);
+int64_t ydbl_lsk_gate_workspace(int32_t n, int32_t h, int32_t w);
+
+/* Adaptive hypergraph (AdaHGConv), tokens = NHWC pixels of view x (D = x.c, N = h*w). */
+typedef struct {
+  ydbl_view x;      /* tokens X (input, also the residual) */
+  ydbl_view xp;     /* pre_head_proj(X), produced by ydbl_conv2d_nhwc */
+  ydbl_view y;      /* output: GELU(node_proj(A @ He)) + X */
+  int32_t num_edges, num_heads;
+  const float* proto_base;  /* [E][D] */
+  const float* ctx_w;       /* [E*D][2D] (context 'both') */
+  const float* ctx_b;       /* [E*D] */
+  const float* edge_w;      /* [D][D] */
+  const float* edge_b;      /* [D] */
+  const float* node_w;      /* [D][D] */
+  const float* node_b;      /* [D] */
+  void* workspace;          /* ydbl_hg_workspace() bytes */
+} ydbl_hg_desc;
+int64_t ydbl_hg_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges);
+/* stage 1: context stats + prototypes (run before the xp GEMM or after; independent of xp) */
+int ydbl_hg_context(const ydbl_hg_desc* d, void* stream);
+/* stage 2: logits, softmax over tokens, vertex->edge->vertex, residual (needs xp) */
+int ydbl_hg_propagate(const ydbl_hg_desc* d, void* stream);
+
+/* Detect decode + NMS candidate extraction.
+ * box[l]: fp32 view [n,h_l,w_l,64] (DFL logits), cls[l]: fp32 view [n,h_l,w_l,nc].
+ * Writes, when y_ref != NULL, the reference output layout y[n][4+nc][A] (xywh pixels, sigmoid).
+ * Candidates per image (cap each): xyxy boxes, score, class, original flat index
+ * (anchor for single-label, anchor*nc+cls for multi-label); cand_count[n] (int32) is
+ * zeroed by this call.  classes/ncls: optional class filter. */
+typedef struct {
+  ydbl_view box[3], cls[3];
+  int32_t nl, nc;
+  float stride[3];
+  float conf_thres;
+  int32_t multi_label;
+  const int32_t* classes; int32_t nclasses;
+  float* y_ref;
+  float* cand_box;     /* [n][cap][4] */
+  float* cand_score;   /* [n][cap] */
+  int32_t* cand_cls;   /* [n][cap] */
+  int32_t* cand_idx;   /* [n][cap] */
+  int32_t* cand_count; /* [n] */
+  int32_t cap;
+} ydbl_decode_desc;
+int ydbl_detect_decode(const ydbl_decode_desc* d, void* stream);
+
+/* NMS candidates straight from a prediction tensor in the reference layout
+ * pred fp32 [n][4+nc][A] (xywh pixels, class scores), as U/utils/ops.py:234-276 reads it.
+ * Same candidate outputs / semantics as ydbl_detect_decode. */
+typedef struct {
+  const float* pred;
+  int32_t n, nc, A;
+  float conf_thres;
+  int32_t multi_label;
+  const int32_t* classes; int32_t nclasses;
+  float* cand_box; float* cand_score; int32_t* cand_cls; int32_t* cand_idx; int32_t* cand_count;
+  int32_t cap;
+} ydbl_pred_cand_desc;
+int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream);
+
+/* Batched class-offset NMS over the candidates of ydbl_detect_decode.
+ * out: fp32 [n][max_det][6] = x1,y1,x2,y2,conf,cls (kept, score order), out_count int32 [n].
+ * Semantics of U/utils/ops.py:278-310 + torchvision nms: candidates above max_nms are cut to the
+ * max_nms highest scores; boxes offset by cls*max_wh (0 if agnostic); stable descending sort;
+ * suppress j if IoU(i,j) > iou_thres (double compare); keep <= max_det.
+ * clip_w/clip_h > 0: clamp kept boxes to [0,w]x[0,h] (scale_boxes with gain 1, pad 0). */
+typedef struct {
+  const float* cand_box; const float* cand_score; const int32_t* cand_cls; const int32_t* cand_idx;
+  const int32_t* cand_count;
+  int32_t n, cap;
+  double iou_thres;
+  int32_t max_det, max_nms, agnostic;
+  float max_wh;
+  float clip_w, clip_h;
+  float* out; int32_t* out_count;
+  void* workspace;
+} ydbl_nms_desc;
+int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms);
+int ydbl_nms(const ydbl_nms_desc* d, void* stream);
+
+const char* ydbl_last_error(void);
+const char* ydbl_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YDBL_H */

@@ -1,0 +1,312 @@
+"""Per-kernel parity on the MI355X: each HIP op vs the oracle / a torch fp32 CPU reference.
+
+Tolerances: fp32 path (exact-f32 MFMA, fp32 VALU) rtol 1e-5-ish, written per test;
+fp16 path: fp16 storage + fp32 accumulation, ~1e-2 relative.  NMS is bit-exact.
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _plan(dtype):
+    from ydbl.runtime import Plan
+
+    return Plan(torch.device(DEV), dtype)
+
+
+def _tv_from_nchw(plan, x, cs_extra=0, c_off=0):
+    """Upload an NCHW CPU tensor into a (possibly channel-sliced) NHWC device view."""
+    from ydbl.runtime import round_up
+
+    n, c, h, w = x.shape
+    cs = round_up(c + c_off + cs_extra, 8)
+    buf = plan.alloc(n, h, w, cs)
+    buf.torch().copy_(torch.zeros(n, h, w, cs, dtype=plan.dtype))
+    v = buf.cslice(c_off, c) if (c_off or cs != c) else buf
+    v.torch().copy_(x.permute(0, 2, 3, 1).to(plan.dtype))
+    return v
+
+
+def _run(plan):
+    plan.run()
+    torch.cuda.synchronize()
+
+
+def _tol(dtype):
+    return dict(rtol=2e-5, atol=2e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin,cout,k,s,act,res", [
+    (8, 16, 3, 1, "silu", None), (16, 32, 3, 2, "silu", None), (64, 64, 3, 1, "silu", "add"),
+    (24, 80, 1, 1, "none", None), (128, 3, 1, 1, "none", None), (32, 48, 1, 1, "silu", "mul"),
+    (96, 144, 3, 2, "silu", None), (8, 8, 3, 1, "silu", None),
+])
+def test_conv_dense(dtype, cin, cout, k, s, act, res):
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin * 1000 + cout + k)
+    n, h, w = 2, 13, 11
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout)
+    ref = F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, s, k // 2)
+    if act == "silu":
+        ref = F.silu(ref)
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)  # read from a channel slice of a wider buffer
+    ho, wo = ref.shape[2:]
+    ybuf = plan.alloc(n, ho, wo, cout + 16)
+    yv = ybuf.cslice(8, cout)  # write into a channel slice
+    rv = None
+    mode = _lib.RES_NONE
+    if res:
+        r = torch.randn(n, cout, ho, wo)
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD if res == "add" else _lib.RES_MUL
+        r = r.to(dtype).float()
+        ref = r + ref if res == "add" else r * ref
+    emit_dense(plan, xv, yv, wt, b, s, k // 2, 1, _lib.ACT_SILU if act == "silu" else _lib.ACT_NONE, rv, mode)
+    _run(plan)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("c,k,s,d,bias,res", [(16, 3, 1, 1, False, False), (32, 3, 2, 1, True, False),
+                                             (64, 7, 1, 1, False, True), (24, 5, 1, 1, True, False),
+                                             (16, 7, 1, 3, True, False)])
+def test_dwconv(dtype, c, k, s, d, bias, res):
+    from ydbl.nn.modules import emit_dw
+
+    torch.manual_seed(c + k)
+    n, h, w = 2, 17, 15
+    x = torch.randn(n, c, h, w)
+    wt = torch.randn(c, 1, k, k) / k
+    b = torch.randn(c) if bias else None
+    p = d * (k - 1) // 2
+    ref = F.conv2d(x.to(dtype).float(), wt, b, s, p, d, groups=c)
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x)
+    ho, wo = ref.shape[2:]
+    yv = plan.alloc(n, ho, wo, c)
+    rv = None
+    if res:
+        r = torch.randn(n, c, ho, wo)
+        rv = _tv_from_nchw(plan, r)
+        ref = r.to(dtype).float() + ref
+    emit_dw(plan, xv, yv, wt, b, s, p, d, res=rv)
+    _run(plan)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
+
+
+def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False):
+    """Run oracle module (CPU fp32) and product module (GPU) on the same inputs/weights."""
+    p_mod.load_state_dict(o_mod.state_dict())
+    with torch.no_grad():
+        ref = o_mod(xs if multi else xs[0])
+    plan = _plan(dtype)
+    views = [_tv_from_nchw(plan, x) for x in xs]
+    out = p_mod.emit(plan, views if multi else views[0])
+    _run(plan)
+    got = out.nchw().float().cpu()
+    torch.testing.assert_close(got, ref, **tol)
+    return got, ref
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_dysample(dtype):
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(3)
+    o = om.DySample(64).eval()
+    with torch.no_grad():
+        o.offset.weight.normal_(0, 0.3)  # offsets large enough to cross pixels and hit the border clamp
+        o.offset.bias.normal_(0, 1.0)
+    x = torch.randn(2, 64, 9, 7)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    _module_parity(o, M.DySample(64), [x], dtype, tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_lskblock(dtype):
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(4)
+    o = om.LSKblock(64).eval()
+    x = torch.randn(2, 64, 12, 10)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    _module_parity(o, M.LSKblock(64), [x], dtype, tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("c,edges", [(64, 4), (128, 8)])
+def test_c3ah_hypergraph(dtype, c, edges):
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(5)
+    o = om.C3AH(c, c, 1, edges).eval()
+    x = torch.randn(2, c, 10, 8)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    _module_parity(o, M.C3AH(c, c, 1, edges), [x], dtype, tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_hyperace(dtype):
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(6)
+    args = (64, 64, 1, 4, True, True, 0.5, 1, "both", True)
+    o = om.HyperACE(*args).eval()
+    xs = [torch.randn(2, 64, 16, 16), torch.randn(2, 64, 8, 8), torch.randn(2, 128, 4, 4)]
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    _module_parity(o, M.HyperACE(*args), xs, dtype, tol, multi=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("name,args,shape", [
+    ("DSC3k2", (32, 32, 2, True), (2, 32, 12, 12)),
+    ("DSC3k2", (32, 48, 1, False), (2, 32, 12, 12)),
+    ("C3Ghost", (64, 64, 2), (2, 64, 10, 10)),
+    ("Bottleneck", (16, 16), (2, 16, 14, 14)),
+    ("DownsampleConv", (32,), (2, 32, 12, 12)),
+])
+def test_blocks(dtype, name, args, shape):
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(7)
+    o = getattr(om, name)(*args).eval()
+    with torch.no_grad():
+        for mod in o.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_var.uniform_(0.5, 2.0)
+                mod.running_mean.normal_(0, 0.1)
+                mod.weight.uniform_(0.5, 1.5)
+                mod.bias.normal_(0, 0.1)
+                mod.eps = 1e-3
+    p = getattr(M, name)(*args)
+    for mod in p.modules():
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.eps = 1e-3
+    # the product folds BN like fuse(); compare against the oracle's fused module
+    from oracle.model import fuse_conv_and_bn
+
+    p.load_state_dict(o.state_dict())
+    for mod in o.modules():
+        if isinstance(mod, om.Conv) and hasattr(mod, "bn"):
+            mod.conv = fuse_conv_and_bn(mod.conv, mod.bn)
+            delattr(mod, "bn")
+    x = torch.randn(*shape)
+    with torch.no_grad():
+        ref = o(x)
+    plan = _plan(dtype)
+    out = p.emit(plan, _tv_from_nchw(plan, x))
+    _run(plan)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(out.nchw().float().cpu(), ref, **tol)
+
+
+# ------------------------------------------------------------------------------------ decode + NMS
+def _decode_inputs(nc, n=2, shapes=((16, 16), (8, 8), (4, 4)), seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(n, 64 + nc, h, w, generator=g) * 2 for h, w in shapes]
+
+
+@pytest.mark.parametrize("nc", [3, 80])
+def test_decode_matches_detect_inference(nc):
+    from oracle import model as om
+    from ydbl import _lib
+    from ydbl.runtime import Plan
+
+    feats = _decode_inputs(nc)
+    d = om.Detect(nc, ch=(16, 16, 16))
+    d.stride = torch.tensor([8.0, 16.0, 32.0])
+    ref = d._inference([f.clone() for f in feats])
+    plan = Plan(torch.device(DEV), torch.float32)
+    levels = [_tv_from_nchw(plan, f) for f in feats]
+    import ctypes as C
+
+    A = sum(f.shape[2] * f.shape[3] for f in feats)
+    yref = torch.empty(2, 4 + nc, A, device=DEV)
+    cap = A * nc
+    cb = torch.empty(2, cap, 4, device=DEV)
+    cs = torch.empty(2, cap, device=DEV)
+    cc = torch.empty(2, cap, dtype=torch.int32, device=DEV)
+    ci = torch.empty(2, cap, dtype=torch.int32, device=DEV)
+    cn = torch.empty(2, dtype=torch.int32, device=DEV)
+    dd = _lib.DecodeDesc((_lib.View * 3)(*[lv.cslice(0, 64).struct() for lv in levels]),
+                         (_lib.View * 3)(*[lv.cslice(64, nc).struct() for lv in levels]), 3, nc,
+                         (C.c_float * 3)(8, 16, 32), 0.5, 1, None, 0, yref.data_ptr(), cb.data_ptr(), cs.data_ptr(),
+                         cc.data_ptr(), ci.data_ptr(), cn.data_ptr(), cap)
+    plan.launch("ydbl_detect_decode", dd, keep=[dd])
+    _run(plan)
+    torch.testing.assert_close(yref.cpu(), ref, rtol=1e-5, atol=1e-4)
+    # candidate set == (anchor, class) pairs with score > 0.5
+    for b in range(2):
+        n = cn[b].item()
+        got = sorted(ci[b, :n].tolist())
+        sc = ref[b, 4:]  # [nc, A]
+        j, a = torch.where(sc > 0.5)
+        assert got == sorted((a * nc + j).tolist())
+
+
+def _rand_pred(n, nc, A, seed, ties=False):
+    g = torch.Generator().manual_seed(seed)
+    xy = torch.rand(n, 2, A, generator=g) * 600 + 20
+    wh = torch.rand(n, 2, A, generator=g) * 120 + 4
+    sc = torch.rand(n, nc, A, generator=g)
+    if ties:
+        sc = (sc * 8).floor() / 8 + 0.01  # many exactly equal scores
+    # clusters of heavily overlapping boxes
+    xy[:, :, ::3] = xy[:, :, 1::3][:, :, : xy[:, :, ::3].shape[2]] + 1.5
+    return torch.cat([xy, wh, sc], 1)
+
+
+@pytest.mark.parametrize("case", [
+    dict(nc=3, A=2000, conf=0.25, iou=0.7, multi=False),
+    dict(nc=3, A=2000, conf=0.25, iou=0.45, multi=False, ties=True),
+    dict(nc=80, A=600, conf=0.3, iou=0.7, multi=True),
+    dict(nc=5, A=9000, conf=0.001, iou=0.6, multi=True),  # > 4096 candidates: global sort + LDS spill path
+    dict(nc=4, A=3000, conf=0.1, iou=0.5, multi=False, agnostic=True),
+    dict(nc=6, A=3000, conf=0.2, iou=0.7, multi=False, classes=[1, 4]),
+    dict(nc=3, A=5000, conf=0.01, iou=0.7, multi=True, max_det=50),
+    dict(nc=3, A=6000, conf=0.01, iou=0.9, multi=True, max_nms=3000),
+    dict(nc=3, A=100, conf=0.999, iou=0.7, multi=False),  # (almost) empty
+])
+def test_nms_bit_exact(case):
+    from oracle.ops import non_max_suppression as ref_nms
+    from ydbl.utils.ops import non_max_suppression
+
+    case = dict(case)
+    nc, A = case.pop("nc"), case.pop("A")
+    pred = _rand_pred(3, nc, A, seed=A + nc, ties=case.pop("ties", False))
+    kw = dict(conf_thres=case["conf"], iou_thres=case["iou"], multi_label=case["multi"],
+              agnostic=case.get("agnostic", False), classes=case.get("classes"), max_det=case.get("max_det", 300),
+              max_nms=case.get("max_nms", 30000))
+    ref = ref_nms(pred.clone(), **kw)
+    got = non_max_suppression(pred.to(DEV), **kw)
+    for r, g in zip(ref, got):
+        assert np.array_equal(g.cpu().numpy(), r.numpy()), (r.shape, g.shape)
+
+
+def test_golden_nms_from_fixture(golden_dir):
+    from ydbl.utils.ops import non_max_suppression
+
+    g = np.load(golden_dir / "golden_n_nc3_128.npz", allow_pickle=False)
+    y = torch.from_numpy(g["y"]).to(DEV)
+    pred = non_max_suppression(y, 0.05, 0.7)
+    val = non_max_suppression(y, 0.001, 0.7, multi_label=True)
+    for i in range(2):
+        assert np.array_equal(pred[i].cpu().numpy(), g[f"pred{i}"])
+        assert np.array_equal(val[i].cpu().numpy(), g[f"val{i}"])

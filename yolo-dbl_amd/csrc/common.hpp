@@ -1,0 +1,139 @@
+// Shared device/host helpers for libydbl (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/ydbl.h"
+
+namespace ydbl {
+
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using h8 = __attribute__((ext_vector_type(8))) _Float16;
+using h4 = __attribute__((ext_vector_type(4))) _Float16;
+
+// ---- error plumbing (thread-local message, int status) -----------------------------------
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+int check_launch(const char* what);
+
+// ---- 16-byte vector of T (8 x f16 or 4 x f32) ---------------------------------------------
+template <typename T> struct Vec;
+template <> struct Vec<_Float16> {
+  static constexpr int N = 8;
+  using type = h8;
+};
+template <> struct Vec<float> {
+  static constexpr int N = 4;
+  using type = f32x4;
+};
+
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type vload(const T* p) {
+  return *reinterpret_cast<const typename Vec<T>::type*>(p);
+}
+template <typename T>
+__device__ __forceinline__ void vstore(T* p, const typename Vec<T>::type& v) {
+  *reinterpret_cast<typename Vec<T>::type*>(p) = v;
+}
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type vzero() {
+  typename Vec<T>::type v;
+#pragma unroll
+  for (int i = 0; i < Vec<T>::N; ++i) v[i] = T(0);
+  return v;
+}
+
+// Load/store VEC elements as fp32.
+template <typename T, int N>
+__device__ __forceinline__ void load_f(const T* p, float* o) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) o[i] = float(p[i]);
+}
+template <int N>
+__device__ __forceinline__ void load_f(const _Float16* p, float* o) {
+  if constexpr (N == 8) {
+    h8 v = *reinterpret_cast<const h8*>(p);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = float(v[i]);
+  } else if constexpr (N == 4) {
+    h4 v = *reinterpret_cast<const h4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = float(v[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) o[i] = float(p[i]);
+  }
+}
+template <int N>
+__device__ __forceinline__ void load_f(const float* p, float* o) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) {
+      f32x4 v = *reinterpret_cast<const f32x4*>(p + i);
+      o[i] = v[0]; o[i + 1] = v[1]; o[i + 2] = v[2]; o[i + 3] = v[3];
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) o[i] = p[i];
+  }
+}
+template <int N>
+__device__ __forceinline__ void store_f(_Float16* p, const float* v) {
+  if constexpr (N == 8) {
+    h8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (_Float16)v[i];
+    *reinterpret_cast<h8*>(p) = o;
+  } else if constexpr (N == 4) {
+    h4 o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) o[i] = (_Float16)v[i];
+    *reinterpret_cast<h4*>(p) = o;
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = (_Float16)v[i];
+  }
+}
+template <int N>
+__device__ __forceinline__ void store_f(float* p, const float* v) {
+  if constexpr (N % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < N; i += 4) *reinterpret_cast<f32x4*>(p + i) = f32x4{v[i], v[i + 1], v[i + 2], v[i + 3]};
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) p[i] = v[i];
+  }
+}
+
+// ---- activations (fp32) ---------------------------------------------------------------------
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float apply_act(float v, int act) {
+  switch (act) {
+    case YDBL_ACT_SILU: return v / (1.0f + expf(-v));
+    case YDBL_ACT_GELU: return gelu_erf(v);
+    case YDBL_ACT_SIGMOID: return sigmoidf_(v);
+    default: return v;
+  }
+}
+
+// Plain-struct view passed by value to kernels.
+template <typename T>
+struct DView {
+  T* p;
+  int n, h, w, c, cs;
+  __device__ __forceinline__ T* at(int b, int y, int x) const { return p + ((int64_t)(b * h + y) * w + x) * cs; }
+  __device__ __forceinline__ T* pix(int64_t pixel) const { return p + pixel * cs; }
+};
+template <typename T>
+inline DView<T> dview(const ydbl_view& v) {
+  return DView<T>{reinterpret_cast<T*>(v.ptr), v.n, v.h, v.w, v.c, v.cs};
+}
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+int check_view(const ydbl_view* v, const char* name, bool need_vec_align);
+
+}  // namespace ydbl

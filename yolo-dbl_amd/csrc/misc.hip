@@ -1,0 +1,393 @@
+// Memory-bound NHWC kernels: depthwise conv, input layout, FullPAD gate, pool/upsample concat,
+// DySample bilinear gather, LSKblock spatial gate.  One thread = one pixel x one 16-byte channel
+// vector (8 x f16 / 4 x f32), fp32 arithmetic, coalesced along channels.
+#include "common.hpp"
+
+namespace ydbl {
+
+// ------------------------------------------------------------------ depthwise convolution
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv_kernel(DView<const T> x, DView<T> y, DView<const T> r,
+                                                     const float* __restrict__ w, const float* __restrict__ bias,
+                                                     int KH, int KW, int S, int PAD, int DIL, int act) {
+  constexpr int V = Vec<T>::N;
+  const int cg = y.c / V;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)y.n * y.h * y.w * cg;
+  if (idx >= total) return;
+  const int c0 = (int)(idx % cg) * V;
+  int64_t pix = idx / cg;
+  const int ox = (int)(pix % y.w);
+  const int64_t t = pix / y.w;
+  const int oy = (int)(t % y.h);
+  const int b = (int)(t / y.h);
+  float acc[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) acc[q] = 0.f;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int iy = oy * S - PAD + ky * DIL;
+    if (iy < 0 || iy >= x.h) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int ix = ox * S - PAD + kx * DIL;
+      if (ix < 0 || ix >= x.w) continue;
+      float xv[V], wv[V];
+      load_f<V>(x.at(b, iy, ix) + c0, xv);
+      load_f<V>(w + (ky * KW + kx) * y.c + c0, wv);
+#pragma unroll
+      for (int q = 0; q < V; ++q) acc[q] = fmaf(xv[q], wv[q], acc[q]);
+    }
+  }
+  if (bias) {
+    float bv[V];
+    load_f<V>(bias + c0, bv);
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] += bv[q];
+  }
+#pragma unroll
+  for (int q = 0; q < V; ++q) acc[q] = apply_act(acc[q], act);
+  if (r.p) {
+    float rv[V];
+    load_f<V>(r.at(b, oy, ox) + c0, rv);
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] = rv[q] + acc[q];
+  }
+  store_f<V>(y.at(b, oy, ox) + c0, acc);
+}
+
+// ------------------------------------------------------------------ input NCHW fp32 -> NHWC
+template <typename T>
+__global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x, int n, int c, int h, int w,
+                                                    float scale, DView<T> y) {
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t hw = (int64_t)h * w;
+  if (pix >= (int64_t)n * hw) return;
+  const int64_t b = pix / hw, off = pix % hw;
+  T* yp = y.pix(pix);
+  for (int c0 = 0; c0 < y.c; c0 += Vec<T>::N) {
+    float v[Vec<T>::N];
+#pragma unroll
+    for (int q = 0; q < Vec<T>::N; ++q) {
+      const int ch = c0 + q;
+      v[q] = ch < c ? x[(b * c + ch) * hw + off] * scale : 0.f;
+    }
+    store_f<Vec<T>::N>(yp + c0, v);
+  }
+}
+
+// ------------------------------------------------------------------ FullPAD: y = a + g * b
+template <typename T>
+__global__ __launch_bounds__(256) void gate_add_kernel(DView<const T> a, DView<const T> bv, float gate, DView<T> y) {
+  constexpr int V = Vec<T>::N;
+  const int cg = y.c / V;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.n * y.h * y.w * cg) return;
+  const int c0 = (int)(idx % cg) * V;
+  const int64_t pix = idx / cg;
+  float av[V], b2[V], o[V];
+  load_f<V>(a.pix(pix) + c0, av);
+  load_f<V>(bv.pix(pix) + c0, b2);
+#pragma unroll
+  for (int q = 0; q < V; ++q) o[q] = av[q] + gate * b2[q];
+  store_f<V>(y.pix(pix) + c0, o);
+}
+
+// ------------------------------------------------------------------ FuseModule / DownsampleConv input
+template <typename T>
+__global__ __launch_bounds__(256) void pool_up_concat_kernel(DView<const T> lo, DView<const T> mid,
+                                                             DView<const T> hi, DView<T> y) {
+  constexpr int V = Vec<T>::N;
+  const int cg = y.c / V;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)y.n * y.h * y.w * cg) return;
+  int c = (int)(idx % cg) * V;
+  const int64_t pix = idx / cg;
+  const int ox = (int)(pix % y.w);
+  const int64_t t = pix / y.w;
+  const int oy = (int)(t % y.h);
+  const int b = (int)(t / y.h);
+  float o[V];
+  const int clo = lo.p ? lo.c : 0, cmid = mid.p ? mid.c : 0;
+  if (c < clo) {  // nn.AvgPool2d(2): mean of the 2x2 window (sum then / 4)
+    float s[V], v[V];
+    load_f<V>(lo.at(b, 2 * oy, 2 * ox) + c, s);
+    load_f<V>(lo.at(b, 2 * oy, 2 * ox + 1) + c, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) s[q] += v[q];
+    load_f<V>(lo.at(b, 2 * oy + 1, 2 * ox) + c, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) s[q] += v[q];
+    load_f<V>(lo.at(b, 2 * oy + 1, 2 * ox + 1) + c, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) o[q] = (s[q] + v[q]) / 4.0f;
+  } else if (c < clo + cmid) {
+    load_f<V>(mid.at(b, oy, ox) + (c - clo), o);
+  } else {  // nn.Upsample(scale_factor=2, mode='nearest')
+    load_f<V>(hi.at(b, oy >> 1, ox >> 1) + (c - clo - cmid), o);
+  }
+  store_f<V>(y.at(b, oy, ox) + c, o);
+}
+
+// ------------------------------------------------------------------ DySample (style lp, scale 2)
+// offset channel k = coord*4G + group*4 + i*2 + j (i,j = sub-pixel row/col of the x2 output).
+// Coordinates follow DySample.py:48-61 and ATen grid_sampler (align_corners=False, border).
+template <typename T>
+__global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<const T> off, int G, DView<T> y) {
+  constexpr int V = Vec<T>::N;
+  const int cpg = x.c / G;
+  const int cgv = cpg / V;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)y.n * y.h * y.w * G * cgv;
+  if (idx >= total) return;
+  const int cv = (int)(idx % cgv);
+  int64_t t = idx / cgv;
+  const int gi = (int)(t % G);
+  t /= G;
+  const int ox2 = (int)(t % y.w);
+  t /= y.w;
+  const int oy2 = (int)(t % y.h);
+  const int b = (int)(t / y.h);
+  const int H = x.h, W = x.w;
+  const int h = oy2 >> 1, w = ox2 >> 1, si = oy2 & 1, sj = ox2 & 1;
+  const T* op = off.at(b, h, w);
+  const float offx = float(op[gi * 4 + si * 2 + sj]);
+  const float offy = float(op[4 * G + gi * 4 + si * 2 + sj]);
+  // normalized grid coordinate, then grid_sampler_unnormalize + border clip
+  const float gx = 2.0f * ((float(w) + 0.5f) + offx) / float(W) - 1.0f;
+  const float gy = 2.0f * ((float(h) + 0.5f) + offy) / float(H) - 1.0f;
+  float ix = ((gx + 1.0f) * float(W) - 1.0f) / 2.0f;
+  float iy = ((gy + 1.0f) * float(H) - 1.0f) / 2.0f;
+  ix = fminf(float(W - 1), fmaxf(ix, 0.0f));
+  iy = fminf(float(H - 1), fmaxf(iy, 0.0f));
+  const int x0 = (int)floorf(ix), y0 = (int)floorf(iy);
+  const int x1 = x0 + 1, y1 = y0 + 1;
+  const float wnw = (float(x1) - ix) * (float(y1) - iy);
+  const float wne = (ix - float(x0)) * (float(y1) - iy);
+  const float wsw = (float(x1) - ix) * (iy - float(y0));
+  const float wse = (ix - float(x0)) * (iy - float(y0));
+  const int c0 = gi * cpg + cv * V;
+  float acc[V], v[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) acc[q] = 0.f;
+  load_f<V>(x.at(b, y0, x0) + c0, v);
+#pragma unroll
+  for (int q = 0; q < V; ++q) acc[q] += v[q] * wnw;
+  if (x1 < W) {
+    load_f<V>(x.at(b, y0, x1) + c0, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] += v[q] * wne;
+  }
+  if (y1 < H) {
+    load_f<V>(x.at(b, y1, x0) + c0, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] += v[q] * wsw;
+  }
+  if (x1 < W && y1 < H) {
+    load_f<V>(x.at(b, y1, x1) + c0, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] += v[q] * wse;
+  }
+  store_f<V>(y.at(b, oy2, ox2) + c0, acc);
+}
+
+// ------------------------------------------------------------------ LSKblock gate
+template <typename T>
+__global__ __launch_bounds__(256) void lsk_stats_kernel(DView<const T> attn, float* __restrict__ agg) {
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (pix >= (int64_t)attn.n * attn.h * attn.w) return;
+  constexpr int V = Vec<T>::N;
+  const T* p = attn.pix(pix);
+  float s = 0.f, m = -INFINITY;
+  for (int c = 0; c < attn.c; c += V) {
+    float v[V];
+    load_f<V>(p + c, v);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      s += v[q];
+      m = fmaxf(m, v[q]);
+    }
+  }
+  agg[pix * 2 + 0] = s / float(attn.c);
+  agg[pix * 2 + 1] = m;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void lsk_gate_kernel(DView<const T> attn, const float* __restrict__ agg,
+                                                       const float* __restrict__ sw, const float* __restrict__ sb,
+                                                       DView<T> out) {
+  constexpr int V = Vec<T>::N;
+  const int half = out.c;
+  const int cg = half / V;
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (int64_t)out.n * out.h * out.w * cg) return;
+  const int c0 = (int)(idx % cg) * V;
+  const int64_t pix = idx / cg;
+  const int ox = (int)(pix % out.w);
+  const int64_t t = pix / out.w;
+  const int oy = (int)(t % out.h);
+  const int b = (int)(t / out.h);
+  float s0 = 0.f, s1 = 0.f;
+  for (int ci = 0; ci < 2; ++ci)
+    for (int ky = 0; ky < 7; ++ky) {
+      const int iy = oy - 3 + ky;
+      if (iy < 0 || iy >= out.h) continue;
+      for (int kx = 0; kx < 7; ++kx) {
+        const int ix = ox - 3 + kx;
+        if (ix < 0 || ix >= out.w) continue;
+        const float a = agg[(((int64_t)b * out.h + iy) * out.w + ix) * 2 + ci];
+        s0 = fmaf(sw[((0 * 2 + ci) * 7 + ky) * 7 + kx], a, s0);
+        s1 = fmaf(sw[((1 * 2 + ci) * 7 + ky) * 7 + kx], a, s1);
+      }
+    }
+  s0 = sigmoidf_(s0 + sb[0]);
+  s1 = sigmoidf_(s1 + sb[1]);
+  float a1[V], a2[V], o[V];
+  load_f<V>(attn.pix(pix) + c0, a1);
+  load_f<V>(attn.pix(pix) + half + c0, a2);
+#pragma unroll
+  for (int q = 0; q < V; ++q) o[q] = a1[q] * s0 + a2[q] * s1;
+  store_f<V>(out.pix(pix) + c0, o);
+}
+
+template <typename T>
+static DView<const T> cview(const ydbl_view* v) {
+  if (!v) return DView<const T>{nullptr, 0, 0, 0, 0, 0};
+  return DView<const T>{reinterpret_cast<const T*>(v->ptr), v->n, v->h, v->w, v->c, v->cs};
+}
+
+static unsigned nblk(int64_t n) { return (unsigned)cdiv(n, 256); }
+
+}  // namespace ydbl
+
+using namespace ydbl;
+
+extern "C" int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream) {
+  if (!d) return fail(YDBL_EINVAL, "dwconv: null descriptor");
+  if (check_view(&d->x, "dwconv.x", true) || check_view(&d->y, "dwconv.y", true)) return YDBL_EINVAL;
+  if (d->x.c != d->y.c || d->x.n != d->y.n || d->x.dtype != d->y.dtype) return fail(YDBL_EINVAL, "dwconv: x/y mismatch");
+  const int ho = (d->x.h + 2 * d->pad - d->dil * (d->kh - 1) - 1) / d->stride + 1;
+  const int wo = (d->x.w + 2 * d->pad - d->dil * (d->kw - 1) - 1) / d->stride + 1;
+  if (ho != d->y.h || wo != d->y.w) return fail(YDBL_EINVAL, "dwconv: output spatial size mismatch");
+  if (!d->w) return fail(YDBL_EINVAL, "dwconv: null weights");
+  const bool res = d->res_mode == YDBL_RES_ADD;
+  if (d->res_mode != YDBL_RES_NONE && !res) return fail(YDBL_EINVAL, "dwconv: only residual ADD is supported");
+  if (res && (check_view(&d->r, "dwconv.r", true) || d->r.c != d->y.c || d->r.n != d->y.n || d->r.h != d->y.h ||
+              d->r.w != d->y.w || d->r.dtype != d->y.dtype))
+    return fail(YDBL_EINVAL, "dwconv: residual shape mismatch");
+  hipStream_t s = as_stream(stream);
+  const int V = d->x.dtype == YDBL_F16 ? 8 : 4;
+  const int64_t total = (int64_t)d->y.n * d->y.h * d->y.w * (d->y.c / V);
+  if (d->x.dtype == YDBL_F16)
+    dwconv_kernel<_Float16><<<nblk(total), 256, 0, s>>>(cview<_Float16>(&d->x), dview<_Float16>(d->y),
+                                                        cview<_Float16>(res ? &d->r : nullptr), d->w, d->bias,
+                                                        d->kh, d->kw, d->stride, d->pad, d->dil, d->act);
+  else
+    dwconv_kernel<float><<<nblk(total), 256, 0, s>>>(cview<float>(&d->x), dview<float>(d->y),
+                                                     cview<float>(res ? &d->r : nullptr), d->w, d->bias, d->kh, d->kw,
+                                                     d->stride, d->pad, d->dil, d->act);
+  return check_launch("ydbl_dwconv2d_nhwc");
+}
+
+extern "C" int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,
+                                       const ydbl_view* y, void* stream) {
+  if (!x) return fail(YDBL_EINVAL, "input: null x");
+  if (check_view(y, "input.y", true)) return YDBL_EINVAL;
+  if (y->n != n || y->h != h || y->w != w || y->c < c) return fail(YDBL_EINVAL, "input: shape mismatch");
+  hipStream_t s = as_stream(stream);
+  const int64_t total = (int64_t)n * h * w;
+  if (y->dtype == YDBL_F16)
+    input_kernel<_Float16><<<nblk(total), 256, 0, s>>>(x, n, c, h, w, scale, dview<_Float16>(*y));
+  else
+    input_kernel<float><<<nblk(total), 256, 0, s>>>(x, n, c, h, w, scale, dview<float>(*y));
+  return check_launch("ydbl_input_nchw_to_nhwc");
+}
+
+extern "C" int ydbl_gate_add(const ydbl_view* a, const ydbl_view* b, float gate, const ydbl_view* y, void* stream) {
+  if (check_view(a, "gate.a", true) || check_view(b, "gate.b", true) || check_view(y, "gate.y", true)) return YDBL_EINVAL;
+  if (a->c != y->c || b->c != y->c || a->n * a->h * a->w != y->n * y->h * y->w ||
+      b->n * b->h * b->w != y->n * y->h * y->w || a->dtype != y->dtype || b->dtype != y->dtype)
+    return fail(YDBL_EINVAL, "gate_add: shape mismatch");
+  hipStream_t s = as_stream(stream);
+  const int V = y->dtype == YDBL_F16 ? 8 : 4;
+  const int64_t total = (int64_t)y->n * y->h * y->w * (y->c / V);
+  if (y->dtype == YDBL_F16)
+    gate_add_kernel<_Float16><<<nblk(total), 256, 0, s>>>(cview<_Float16>(a), cview<_Float16>(b), gate, dview<_Float16>(*y));
+  else
+    gate_add_kernel<float><<<nblk(total), 256, 0, s>>>(cview<float>(a), cview<float>(b), gate, dview<float>(*y));
+  return check_launch("ydbl_gate_add");
+}
+
+extern "C" int ydbl_pool_up_concat(const ydbl_view* lo, const ydbl_view* mid, const ydbl_view* hi, const ydbl_view* y,
+                                   void* stream) {
+  if (check_view(y, "concat.y", true)) return YDBL_EINVAL;
+  int ctot = 0;
+  if (lo) {
+    if (check_view(lo, "concat.lo", true)) return YDBL_EINVAL;
+    if (lo->h != 2 * y->h || lo->w != 2 * y->w || lo->n != y->n) return fail(YDBL_EINVAL, "concat: lo must be 2x output");
+    ctot += lo->c;
+  }
+  if (mid) {
+    if (check_view(mid, "concat.mid", true)) return YDBL_EINVAL;
+    if (mid->h != y->h || mid->w != y->w || mid->n != y->n) return fail(YDBL_EINVAL, "concat: mid must match output");
+    ctot += mid->c;
+  }
+  if (hi) {
+    if (check_view(hi, "concat.hi", true)) return YDBL_EINVAL;
+    if (2 * hi->h != y->h || 2 * hi->w != y->w || hi->n != y->n) return fail(YDBL_EINVAL, "concat: hi must be 1/2 output");
+    ctot += hi->c;
+  }
+  if (ctot != y->c) return fail(YDBL_EINVAL, "concat: channel sum mismatch");
+  hipStream_t s = as_stream(stream);
+  const int V = y->dtype == YDBL_F16 ? 8 : 4;
+  const int64_t total = (int64_t)y->n * y->h * y->w * (y->c / V);
+  if (y->dtype == YDBL_F16)
+    pool_up_concat_kernel<_Float16><<<nblk(total), 256, 0, s>>>(cview<_Float16>(lo), cview<_Float16>(mid),
+                                                                 cview<_Float16>(hi), dview<_Float16>(*y));
+  else
+    pool_up_concat_kernel<float><<<nblk(total), 256, 0, s>>>(cview<float>(lo), cview<float>(mid), cview<float>(hi),
+                                                              dview<float>(*y));
+  return check_launch("ydbl_pool_up_concat");
+}
+
+extern "C" int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y,
+                             void* stream) {
+  if (check_view(x, "dysample.x", true) || check_view(off, "dysample.off", false) || check_view(y, "dysample.y", true))
+    return YDBL_EINVAL;
+  const int V = y->dtype == YDBL_F16 ? 8 : 4;
+  if (groups < 1 || x->c % groups || (x->c / groups) % V) return fail(YDBL_EINVAL, "dysample: bad groups");
+  if (off->c != 8 * groups || off->h != x->h || off->w != x->w || y->h != 2 * x->h || y->w != 2 * x->w ||
+      y->c != x->c || off->dtype != x->dtype || y->dtype != x->dtype)
+    return fail(YDBL_EINVAL, "dysample: shape mismatch");
+  hipStream_t s = as_stream(stream);
+  const int64_t total = (int64_t)y->n * y->h * y->w * groups * (x->c / groups / V);
+  if (y->dtype == YDBL_F16)
+    dysample_kernel<_Float16><<<nblk(total), 256, 0, s>>>(cview<_Float16>(x), cview<_Float16>(off), groups,
+                                                           dview<_Float16>(*y));
+  else
+    dysample_kernel<float><<<nblk(total), 256, 0, s>>>(cview<float>(x), cview<float>(off), groups, dview<float>(*y));
+  return check_launch("ydbl_dysample");
+}
+
+extern "C" int64_t ydbl_lsk_gate_workspace(int32_t n, int32_t h, int32_t w) { return (int64_t)n * h * w * 2 * 4; }
+
+extern "C" int ydbl_lsk_gate(const ydbl_view* attn, const float* sw, const float* sb, const ydbl_view* out,
+                             void* workspace, void* stream) {
+  if (check_view(attn, "lsk.attn", true) || check_view(out, "lsk.out", true)) return YDBL_EINVAL;
+  if (attn->c != 2 * out->c || attn->n != out->n || attn->h != out->h || attn->w != out->w ||
+      attn->dtype != out->dtype)
+    return fail(YDBL_EINVAL, "lsk: shape mismatch");
+  if (!sw || !sb || !workspace) return fail(YDBL_EINVAL, "lsk: null weights/workspace");
+  hipStream_t s = as_stream(stream);
+  float* agg = reinterpret_cast<float*>(workspace);
+  const int64_t npix = (int64_t)out->n * out->h * out->w;
+  const int V = out->dtype == YDBL_F16 ? 8 : 4;
+  if (out->dtype == YDBL_F16) {
+    lsk_stats_kernel<_Float16><<<nblk(npix), 256, 0, s>>>(cview<_Float16>(attn), agg);
+    lsk_gate_kernel<_Float16><<<nblk(npix * (out->c / V)), 256, 0, s>>>(cview<_Float16>(attn), agg, sw, sb,
+                                                                         dview<_Float16>(*out));
+  } else {
+    lsk_stats_kernel<float><<<nblk(npix), 256, 0, s>>>(cview<float>(attn), agg);
+    lsk_gate_kernel<float><<<nblk(npix * (out->c / V)), 256, 0, s>>>(cview<float>(attn), agg, sw, sb,
+                                                                      dview<float>(*out));
+  }
+  return check_launch("ydbl_lsk_gate");
+}

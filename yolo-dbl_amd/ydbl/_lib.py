@@ -1,0 +1,131 @@
+"""ctypes binding of libydbl.so (the C ABI in include/ydbl.h).
+
+There is no fallback: if the library is missing or cannot be loaded the
+import raises, so a GPU run can never silently go through another path.
+torch is imported first so that libydbl resolves ``libamdhip64.so.7`` to the
+HIP runtime torch already loaded (one runtime, one set of streams).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the dlopen below)
+
+LIB_PATH = Path(os.environ.get("YDBL_LIB", Path(__file__).resolve().parent / "libydbl.so"))
+
+F32, F16 = 0, 1
+ACT_NONE, ACT_SILU, ACT_GELU, ACT_SIGMOID = 0, 1, 2, 3
+RES_NONE, RES_ADD, RES_MUL = 0, 1, 2
+
+
+class View(C.Structure):
+    _fields_ = [("ptr", C.c_void_p), ("n", C.c_int32), ("h", C.c_int32), ("w", C.c_int32), ("c", C.c_int32),
+                ("cs", C.c_int32), ("dtype", C.c_int32)]
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [("x", View), ("y", View), ("r", View), ("w", C.c_void_p), ("bias", C.c_void_p),
+                ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32), ("dil", C.c_int32),
+                ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32)]
+
+
+class DwConvDesc(C.Structure):
+    _fields_ = [("x", View), ("y", View), ("r", View), ("w", C.c_void_p), ("bias", C.c_void_p),
+                ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32), ("dil", C.c_int32),
+                ("act", C.c_int32), ("res_mode", C.c_int32)]
+
+
+class HgDesc(C.Structure):
+    _fields_ = [("x", View), ("xp", View), ("y", View), ("num_edges", C.c_int32), ("num_heads", C.c_int32),
+                ("proto_base", C.c_void_p), ("ctx_w", C.c_void_p), ("ctx_b", C.c_void_p),
+                ("edge_w", C.c_void_p), ("edge_b", C.c_void_p), ("node_w", C.c_void_p), ("node_b", C.c_void_p),
+                ("workspace", C.c_void_p)]
+
+
+class DecodeDesc(C.Structure):
+    _fields_ = [("box", View * 3), ("cls", View * 3), ("nl", C.c_int32), ("nc", C.c_int32),
+                ("stride", C.c_float * 3), ("conf_thres", C.c_float), ("multi_label", C.c_int32),
+                ("classes", C.c_void_p), ("nclasses", C.c_int32), ("y_ref", C.c_void_p),
+                ("cand_box", C.c_void_p), ("cand_score", C.c_void_p), ("cand_cls", C.c_void_p),
+                ("cand_idx", C.c_void_p), ("cand_count", C.c_void_p), ("cap", C.c_int32)]
+
+
+class PredCandDesc(C.Structure):
+    _fields_ = [("pred", C.c_void_p), ("n", C.c_int32), ("nc", C.c_int32), ("A", C.c_int32),
+                ("conf_thres", C.c_float), ("multi_label", C.c_int32), ("classes", C.c_void_p),
+                ("nclasses", C.c_int32), ("cand_box", C.c_void_p), ("cand_score", C.c_void_p),
+                ("cand_cls", C.c_void_p), ("cand_idx", C.c_void_p), ("cand_count", C.c_void_p), ("cap", C.c_int32)]
+
+
+class NmsDesc(C.Structure):
+    _fields_ = [("cand_box", C.c_void_p), ("cand_score", C.c_void_p), ("cand_cls", C.c_void_p),
+                ("cand_idx", C.c_void_p), ("cand_count", C.c_void_p), ("n", C.c_int32), ("cap", C.c_int32),
+                ("iou_thres", C.c_double), ("max_det", C.c_int32), ("max_nms", C.c_int32), ("agnostic", C.c_int32),
+                ("max_wh", C.c_float), ("clip_w", C.c_float), ("clip_h", C.c_float), ("out", C.c_void_p),
+                ("out_count", C.c_void_p), ("workspace", C.c_void_p)]
+
+
+# name -> (argtypes, restype); every entry must exist in include/ydbl.h
+_P = C.c_void_p
+_VP = C.POINTER(View)
+SIGNATURES = {
+    "ydbl_conv2d_nhwc": ([C.POINTER(ConvDesc), _P], C.c_int),
+    "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
+    "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
+    "ydbl_gate_add": ([_VP, _VP, C.c_float, _VP, _P], C.c_int),
+    "ydbl_pool_up_concat": ([_VP, _VP, _VP, _VP, _P], C.c_int),
+    "ydbl_dysample": ([_VP, _VP, C.c_int32, _VP, _P], C.c_int),
+    "ydbl_lsk_gate": ([_VP, _P, _P, _VP, _P, _P], C.c_int),
+    "ydbl_lsk_gate_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_hg_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_hg_context": ([C.POINTER(HgDesc), _P], C.c_int),
+    "ydbl_hg_propagate": ([C.POINTER(HgDesc), _P], C.c_int),
+    "ydbl_detect_decode": ([C.POINTER(DecodeDesc), _P], C.c_int),
+    "ydbl_pred_candidates": ([C.POINTER(PredCandDesc), _P], C.c_int),
+    "ydbl_nms_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_nms": ([C.POINTER(NmsDesc), _P], C.c_int),
+    "ydbl_last_error": ([], C.c_char_p),
+    "ydbl_version": ([], C.c_char_p),
+}
+
+
+def _load():
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"libydbl.so not found at {LIB_PATH}; build it with `python -c \"import __graft_entry__ as g; g.build()\"` "
+            "(the HIP path has no fallback)"
+        )
+    lib = C.CDLL(str(LIB_PATH))
+    for name, (args, res) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+lib = _load()
+
+
+class YdblError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        msg = lib.ydbl_last_error().decode(errors="replace")
+        raise YdblError(f"{what or 'ydbl'} failed (code {rc}): {msg}")
+
+
+def dtype_code(dt: torch.dtype) -> int:
+    if dt == torch.float16:
+        return F16
+    if dt == torch.float32:
+        return F32
+    raise TypeError(f"unsupported activation dtype {dt}")
+
+
+def version() -> str:
+    return lib.ydbl_version().decode()

@@ -1,0 +1,173 @@
+"""User API: ``YOLO(cfg_or_weights)`` with ``.predict()``, ``.val()``, ``.fuse()``.
+
+Mirrors U/engine/model.py:84-643 and U/models/yolo/model.py:52-100 for the
+detect task: model files named like the reference's
+(``yolov13n_DBL.yaml`` / ``yolov13s_DBL.yaml`` / ``yolov13l_DBL2.yaml``) build
+the same layer graph; ``predict`` keeps the reference's argument names and
+defaults (conf 0.25, iou 0.7, max_det 300, half False, agnostic_nms, classes;
+U/cfg/default.yaml:51-54 and U/engine/model.py:547) and returns ``Results``.
+Everything after construction runs on the GPU through libydbl; there is no CPU
+execution path (``device='cpu'`` raises).
+"""
+
+from __future__ import annotations
+
+import time
+from pathlib import Path
+
+import torch
+
+from ..nn.tasks import DetectionModel
+from .results import Results
+from .session import DetectSession
+
+DEFAULTS = {"conf": 0.25, "iou": 0.7, "max_det": 300, "half": False, "device": None, "agnostic_nms": False,
+            "classes": None, "batch": 1, "verbose": False}
+
+
+def select_device(device=None) -> torch.device:
+    """U/utils/torch_utils.py select_device, GPU-only."""
+    if device is None or device == "":
+        device = 0
+    if isinstance(device, torch.device):
+        dev = device
+    elif isinstance(device, int):
+        dev = torch.device("cuda", device)
+    else:
+        s = str(device).lower().replace("cuda:", "").strip()
+        if s == "cpu":
+            raise RuntimeError("ydbl runs on MI355X (gfx950) only; device='cpu' has no implementation")
+        dev = torch.device("cuda", int(s.split(",")[0]) if s else 0)
+    if dev.type != "cuda":
+        raise RuntimeError(f"ydbl runs on MI355X (gfx950) only; got device {dev}")
+    if not torch.cuda.is_available():
+        raise RuntimeError("no GPU visible: ydbl has no CPU fallback")
+    return dev
+
+
+def load_tensor_source(im: torch.Tensor, stride: int = 32) -> torch.Tensor:
+    """LoadTensor._single_check (U/data/loaders.py:515-580): BCHW, H and W divisible by the stride, /255 if >1."""
+    if isinstance(im, (list, tuple)):
+        im = torch.stack([t if t.ndim == 3 else t[0] for t in im])
+    if not isinstance(im, torch.Tensor):
+        raise TypeError(f"ydbl predict() takes torch tensors (BCHW float); got {type(im).__name__}")
+    if im.ndim == 3:
+        im = im.unsqueeze(0)
+    if im.ndim != 4 or im.shape[1] != 3:
+        raise ValueError(f"torch.Tensor inputs should be BCHW i.e. shape(b, 3, h, w) but got {tuple(im.shape)}")
+    if im.shape[2] % stride or im.shape[3] % stride:
+        raise ValueError(
+            f"torch.Tensor inputs should be BCHW with height and width divisible by stride {stride}; got {tuple(im.shape)}")
+    if im.max() > 1.0 + torch.finfo(im.dtype).eps:
+        im = im.float() / 255.0
+    return im
+
+
+class Model:
+    """U/engine/model.py:84-643 (detect task subset)."""
+
+    def __init__(self, model: str | Path = "yolov13n_DBL.yaml", task=None, verbose=False, nc=None):
+        self.task = task or "detect"
+        self.overrides = {}
+        self.ckpt_path = None
+        self.verbose = verbose
+        self._sessions = {}
+        model = str(model)
+        suffix = Path(model).suffix.lower()
+        if suffix in (".pt", ".pth", ".safetensors"):
+            raise ValueError("build from a config and call .load(weights): YOLO('yolov13n_DBL.yaml').load('w.pt')")
+        self.model = DetectionModel(model, nc=nc, verbose=verbose)
+        self.cfg = model
+        self.overrides["model"] = model
+
+    # ------------------------------------------------------------------ weights
+    def load(self, weights):
+        """Load a state_dict (torch weights_only file, safetensors, or a dict) with the reference's key names."""
+        if isinstance(weights, dict):
+            sd = weights
+        elif str(weights).endswith(".safetensors"):
+            from safetensors.torch import load_file
+
+            sd = load_file(str(weights))
+        else:
+            obj = torch.load(str(weights), map_location="cpu", weights_only=True)
+            sd = obj.get("state_dict", obj.get("model", obj)) if isinstance(obj, dict) else obj
+            if not isinstance(sd, dict):
+                raise ValueError("weights file must hold a state_dict")
+        sd = {k[len("model."):] if k.startswith("model.model.") else k: v for k, v in sd.items()}
+        missing, unexpected = self.model.load_state_dict(sd, strict=False)
+        if unexpected:
+            raise KeyError(f"unexpected keys in weights: {unexpected[:5]} ...")
+        self._sessions.clear()
+        self.ckpt_path = str(weights) if not isinstance(weights, dict) else None
+        return self
+
+    def state_dict(self):
+        return self.model.state_dict()
+
+    @property
+    def names(self):
+        return self.model.names
+
+    @property
+    def stride(self):
+        return self.model.stride
+
+    def fuse(self):
+        self.model.fuse()
+        return self
+
+    def info(self):
+        n = sum(p.numel() for p in self.model.parameters())
+        return {"layers": len(self.model.model), "parameters": n}
+
+    # ------------------------------------------------------------------ inference
+    def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
+                multi_label=False, device=None, keep_pred=False, use_graph=True) -> DetectSession:
+        dev = select_device(device)
+        dtype = torch.float16 if half else torch.float32
+        key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
+               tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph)
+        s = self._sessions.get(key)
+        if s is None:
+            with torch.cuda.device(dev):
+                s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
+                                  keep_pred=keep_pred, use_graph=use_graph, device=dev)
+            self._sessions[key] = s
+        return s
+
+    def predict(self, source=None, stream=False, **kwargs):
+        """U/engine/model.py:501-560 + DetectionPredictor.postprocess (U/models/yolo/detect/predict.py:23-41)."""
+        args = {**DEFAULTS, **self.overrides, **kwargs}
+        dev = select_device(args["device"])
+        t0 = time.perf_counter()
+        im = load_tensor_source(source, int(self.model.stride.max()))
+        im = im.to(dev, non_blocking=True).float()
+        b, _, h, w = im.shape
+        s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
+                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev)
+        t1 = time.perf_counter()
+        det, cnt = s(im)
+        counts = cnt.tolist()  # one sync per batch
+        t2 = time.perf_counter()
+        speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b, "postprocess": 0.0}
+        results = [Results(im[i].permute(1, 2, 0), path=f"image{i}.jpg", names=self.model.names,
+                           boxes=det[i, : counts[i]].clone(), speed=speed) for i in range(b)]
+        return iter(results) if stream else results
+
+    __call__ = predict
+
+    def val(self, data=None, **kwargs):
+        """Detection mAP on an in-memory dataset; see ydbl.engine.validator."""
+        from .validator import DetectionValidator
+
+        args = {**DEFAULTS, "conf": 0.001, "iou": 0.7, "batch": 16, **kwargs}
+        return DetectionValidator(self, args)(data)
+
+
+class YOLO(Model):
+    """U/models/yolo/model.py:52-100 — detect task only."""
+
+    @property
+    def task_map(self):
+        return {"detect": {"model": DetectionModel, "predictor": DetectSession}}

@@ -1,0 +1,96 @@
+"""One compiled inference configuration: forward + Detect decode + NMS as a single launch plan.
+
+The plan is captured into a hipGraph on first use and replayed afterwards, so
+a batch costs one H2D/D2D copy into the static input buffer plus one graph
+launch.  Outputs are fixed-shape device buffers ``det [B, max_det, 6]``
+(x1, y1, x2, y2, conf, cls) and ``count [B]`` — the all-gather friendly
+layout used by the multi-GPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from .. import _lib
+from .._lib import DecodeDesc, NmsDesc, View
+from ..runtime import GraphRunner, Plan
+
+
+class DetectSession:
+    def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
+                 multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
+                 keep_pred=False, use_graph=True, device="cuda"):
+        self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
+        self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
+        cm = model.compile(batch, h, w, dtype, device=device)
+        self.compiled = cm
+        plan: Plan = cm.plan
+        det = cm.detect
+        nc = det.nc
+        multi_label = bool(multi_label) and nc > 1
+        A = sum(lv.h * lv.w for lv in cm.levels)
+        self.A, self.nc = A, nc
+        cap = A * nc if multi_label else A
+        dev = plan.device
+        self.cand_box = torch.empty((batch, cap, 4), dtype=torch.float32, device=dev)
+        self.cand_score = torch.empty((batch, cap), dtype=torch.float32, device=dev)
+        self.cand_cls = torch.empty((batch, cap), dtype=torch.int32, device=dev)
+        self.cand_idx = torch.empty((batch, cap), dtype=torch.int32, device=dev)
+        self.cand_count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+        self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
+        self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
+        self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+        self.classes_t = (torch.tensor(list(classes), dtype=torch.int32, device=dev) if classes is not None else None)
+        ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(batch, cap, max_nms)), dtype=torch.uint8, device=dev)
+        plan.buffers += [self.cand_box, self.cand_score, self.cand_cls, self.cand_idx, self.cand_count, self.det,
+                         self.count, ws]
+        boxes = (View * 3)(*[lv.cslice(0, 64).struct() for lv in cm.levels])
+        clss = (View * 3)(*[lv.cslice(64, nc).struct() for lv in cm.levels])
+        strides = (C.c_float * 3)(*[float(s) for s in det.stride.tolist()])
+        dd = DecodeDesc(boxes, clss, len(cm.levels), nc, strides, self.conf, int(multi_label),
+                        self.classes_t.data_ptr() if self.classes_t is not None else None,
+                        len(self.classes_t) if self.classes_t is not None else 0,
+                        self.pred.data_ptr() if self.pred is not None else None,
+                        self.cand_box.data_ptr(), self.cand_score.data_ptr(), self.cand_cls.data_ptr(),
+                        self.cand_idx.data_ptr(), self.cand_count.data_ptr(), cap)
+        plan.launch("ydbl_detect_decode", dd, what="Detect.decode", keep=[dd])
+        nd = NmsDesc(self.cand_box.data_ptr(), self.cand_score.data_ptr(), self.cand_cls.data_ptr(),
+                     self.cand_idx.data_ptr(), self.cand_count.data_ptr(), batch, cap, self.iou, self.max_det,
+                     int(max_nms), int(bool(agnostic)), float(max_wh), float(w) if clip else 0.0,
+                     float(h) if clip else 0.0, self.det.data_ptr(), self.count.data_ptr(), ws.data_ptr())
+        plan.launch("ydbl_nms", nd, what="NMS", keep=[nd])
+        self.plan = plan
+        self.use_graph = use_graph
+        self._graph = None
+
+    # ------------------------------------------------------------------ execution
+    def load(self, x: torch.Tensor):
+        """Copy a BCHW float batch into the static input buffer (LoadTensor semantics are the caller's)."""
+        if tuple(x.shape) != tuple(self.compiled.input.shape):
+            raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
+        self.compiled.input.copy_(x, non_blocking=True)
+
+    def launch(self):
+        if self.use_graph:
+            if self._graph is None:
+                self._graph = GraphRunner(self.plan)
+            self._graph.replay()
+        else:
+            self.plan.run()
+
+    def __call__(self, x: torch.Tensor | None = None):
+        if x is not None:
+            self.load(x)
+        self.launch()
+        return self.det, self.count
+
+    def results(self):
+        """Host list of [n_i, 6] tensors (one sync)."""
+        cnt = self.count.cpu().tolist()
+        det = self.det.cpu()
+        return [det[i, : cnt[i]].clone() for i in range(self.batch)]
+
+    def feats(self):
+        return self.compiled.feats()

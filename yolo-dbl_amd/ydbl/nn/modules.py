@@ -1,0 +1,653 @@
+"""YOLO-DBL building blocks, MI355X path.
+
+Each class keeps the reference's constructor signature, submodule names and
+parameter shapes (so ``parse_model`` resolves the DBL YAMLs by class name and
+reference ``state_dict`` keys load unchanged), but instead of a torch
+``forward`` it ``emit``s HIP launches into a ``Plan``:
+
+    y = module.emit(plan, x, out=None)   # x, y: NHWC TV views (lists for multi-input)
+
+``out`` (optional) is a destination view, typically a channel slice of a
+concat buffer, so Concat / chunk / C2f / C3 concatenations cost no copies.
+BatchNorm is folded exactly as ``fuse_conv_and_bn`` does
+(U/utils/torch_utils.py:238-265); DSConv's BN (left unfused by the reference,
+U/nn/tasks.py:217) is folded into its pointwise conv here.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .._lib import ConvDesc, DwConvDesc, HgDesc, View
+from ..runtime import TV, Plan, round_up
+
+
+# =============================================================================== weight prep + launches
+def autopad(k, p=None, d=1):
+    """U/nn/modules/conv.py:30-36."""
+    if d > 1:
+        k = d * (k - 1) + 1 if isinstance(k, int) else [d * (x - 1) + 1 for x in k]
+    if p is None:
+        p = k // 2 if isinstance(k, int) else [x // 2 for x in k]
+    return p
+
+
+@torch.no_grad()
+def fold_bn(weight: torch.Tensor, bias: torch.Tensor | None, bn: nn.BatchNorm2d):
+    """Same op sequence as fuse_conv_and_bn (diag-matrix products), fp32 on the host."""
+    w = weight.detach().float().cpu()
+    co = w.shape[0]
+    w_bn = torch.diag(bn.weight.detach().float().cpu().div(torch.sqrt(bn.eps + bn.running_var.float().cpu())))
+    wf = torch.mm(w_bn, w.view(co, -1)).view(w.shape)
+    b_conv = torch.zeros(co) if bias is None else bias.detach().float().cpu()
+    b_bn = bn.bias.detach().float().cpu() - bn.weight.detach().float().cpu().mul(
+        bn.running_mean.float().cpu()
+    ).div(torch.sqrt(bn.running_var.float().cpu() + bn.eps))
+    bf = torch.mm(w_bn, b_conv.reshape(-1, 1)).reshape(-1) + b_bn
+    return wf, bf
+
+
+def _act_code(act) -> int:
+    if isinstance(act, nn.SiLU):
+        return _lib.ACT_SILU
+    if isinstance(act, nn.GELU):
+        return _lib.ACT_GELU
+    if isinstance(act, nn.Identity) or act is None:
+        return _lib.ACT_NONE
+    raise NotImplementedError(f"activation {type(act).__name__} has no HIP epilogue")
+
+
+def _null_view() -> View:
+    return View(None, 0, 0, 0, 0, 0, 0)
+
+
+def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,
+               act=_lib.ACT_NONE, res: TV | None = None, res_mode=_lib.RES_NONE, what="conv"):
+    """Dense conv y = act(conv(x) + b) [+/* res]; w fp32 [co, ci, kh, kw] (ci may be < x.c: zero-padded)."""
+    co, ci, kh, kw = w.shape
+    assert ci <= x.c and co == y.c, (w.shape, x.shape, y.shape)
+    wt = w.permute(0, 2, 3, 1)
+    if ci < x.c:
+        wt = torch.nn.functional.pad(wt, (0, x.c - ci))
+    K = kh * kw * x.c
+    kpad = round_up(K, 32)
+    wk = torch.nn.functional.pad(wt.reshape(co, K), (0, kpad - K)).to(plan.dtype)
+    wd = plan.const(wk)
+    bd = plan.const(b.float()) if b is not None else None
+    d = ConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(), wd.data_ptr(),
+                 bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, kpad, act, res_mode)
+    plan.launch("ydbl_conv2d_nhwc", d, what=what, keep=[wd, bd, d])
+
+
+def emit_dw(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,
+            act=_lib.ACT_NONE, res: TV | None = None, what="dwconv"):
+    """Depthwise conv; w fp32 [c, 1, kh, kw]."""
+    c, _, kh, kw = w.shape
+    assert c == x.c == y.c
+    wd = plan.const(w.float().reshape(c, kh * kw).t().contiguous())
+    bd = plan.const(b.float()) if b is not None else None
+    d = DwConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(), wd.data_ptr(),
+                   bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, act,
+                   _lib.RES_ADD if res is not None else _lib.RES_NONE)
+    plan.launch("ydbl_dwconv2d_nhwc", d, what=what, keep=[wd, bd, d])
+
+
+def conv_out_hw(h, w, k, s, p, d):
+    return (h + 2 * p - d * (k - 1) - 1) // s + 1, (w + 2 * p - d * (k - 1) - 1) // s + 1
+
+
+def emit_conv2d(plan: Plan, conv: nn.Conv2d, x: TV, out: TV | None, weight=None, bias=None, act=_lib.ACT_NONE,
+                res: TV | None = None, res_mode=_lib.RES_NONE, what="conv") -> TV:
+    """Launch an nn.Conv2d (dense or depthwise) with optional replacement weight/bias."""
+    k, s, p, d = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.dilation[0]
+    assert conv.kernel_size[0] == conv.kernel_size[1] and conv.stride[0] == conv.stride[1]
+    w = (conv.weight if weight is None else weight).detach().float().cpu()
+    b = bias if bias is not None else (conv.bias.detach().float().cpu() if conv.bias is not None else None)
+    ho, wo = conv_out_hw(x.h, x.w, k, s, p, d)
+    y = out if out is not None else plan.alloc(x.n, ho, wo, conv.out_channels)
+    assert (y.h, y.w, y.c) == (ho, wo, conv.out_channels), ((y.h, y.w, y.c), (ho, wo, conv.out_channels))
+    if conv.groups == 1:
+        emit_dense(plan, x, y, w, b, s, p, d, act, res, res_mode, what)
+    elif conv.groups == conv.in_channels == conv.out_channels:
+        if res_mode not in (_lib.RES_NONE, _lib.RES_ADD):
+            raise NotImplementedError("depthwise conv supports residual ADD only")
+        emit_dw(plan, x, y, w, b, s, p, d, act, res if res_mode == _lib.RES_ADD else None, what)
+    else:
+        raise NotImplementedError(f"grouped conv g={conv.groups} is not on the DBL path")
+    return y
+
+
+def emit_seq(plan: Plan, mods, x, out=None):
+    mods = list(mods)
+    for i, m in enumerate(mods):
+        x = m.emit(plan, x, out if i == len(mods) - 1 else None)
+    return x
+
+
+def emit_copy(plan: Plan, src: TV, dst: TV):
+    plan.launch("ydbl_pool_up_concat", None, src.struct(), None, dst.struct(), what="copy")
+
+
+# =============================================================================== conv.py
+class Conv(nn.Module):
+    """U/nn/modules/conv.py:39-63 — conv -> BN -> SiLU (BN folded at plan time, as fuse() does)."""
+
+    default_act = nn.SiLU()
+
+    def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, c2, k, s, autopad(k, p, d), groups=g, dilation=d, bias=False)
+        self.bn = nn.BatchNorm2d(c2)
+        self.act = self.default_act if act is True else act if isinstance(act, nn.Module) else nn.Identity()
+
+    def folded(self):
+        if hasattr(self, "bn"):
+            return fold_bn(self.conv.weight, self.conv.bias, self.bn)
+        return self.conv.weight.detach().float().cpu(), (
+            self.conv.bias.detach().float().cpu() if self.conv.bias is not None else None)
+
+    def emit(self, plan, x, out=None, res=None, res_mode=_lib.RES_NONE):
+        w, b = self.folded()
+        return emit_conv2d(plan, self.conv, x, out, w, b, _act_code(self.act), res, res_mode,
+                           what=f"Conv{self.conv.kernel_size[0]}x{self.conv.kernel_size[0]}")
+
+
+class DWConv(Conv):
+    """U/nn/modules/conv.py:128-133."""
+
+    def __init__(self, c1, c2, k=1, s=1, d=1, act=True):
+        super().__init__(c1, c2, k, s, g=math.gcd(c1, c2), d=d, act=act)
+
+
+class DSConv(nn.Module):
+    """U/nn/modules/conv.py:91-108 — dw -> pw -> BN -> SiLU."""
+
+    def __init__(self, c_in, c_out, k=3, s=1, p=None, d=1, bias=False):
+        super().__init__()
+        if p is None:
+            p = (d * (k - 1)) // 2
+        self.dw = nn.Conv2d(c_in, c_in, kernel_size=k, stride=s, padding=p, dilation=d, groups=c_in, bias=bias)
+        self.pw = nn.Conv2d(c_in, c_out, 1, 1, 0, bias=bias)
+        self.bn = nn.BatchNorm2d(c_out)
+        self.act = nn.SiLU()
+
+    def emit(self, plan, x, out=None, res=None, res_mode=_lib.RES_NONE):
+        t = emit_conv2d(plan, self.dw, x, None, what=f"DSConv.dw{self.dw.kernel_size[0]}")
+        w, b = fold_bn(self.pw.weight, self.pw.bias, self.bn)
+        return emit_conv2d(plan, self.pw, t, out, w, b, _lib.ACT_SILU, res, res_mode, what="DSConv.pw")
+
+
+class GhostConv(nn.Module):
+    """U/nn/modules/conv.py:184-197 — cat(y, dw5x5(y)), y = cv1(x)."""
+
+    def __init__(self, c1, c2, k=1, s=1, g=1, act=True):
+        super().__init__()
+        c_ = c2 // 2
+        self.cv1 = Conv(c1, c_, k, s, None, g, act=act)
+        self.cv2 = Conv(c_, c_, 5, 1, None, c_, act=act)
+
+    def emit(self, plan, x, out=None, res=None):
+        c_ = self.cv1.conv.out_channels
+        ho, wo = conv_out_hw(x.h, x.w, self.cv1.conv.kernel_size[0], self.cv1.conv.stride[0],
+                             self.cv1.conv.padding[0], 1)
+        y = out if out is not None else plan.alloc(x.n, ho, wo, 2 * c_)
+        r0 = res.cslice(0, c_) if res is not None else None
+        r1 = res.cslice(c_, c_) if res is not None else None
+        # the dw half reads the pre-residual cv1 output, so with a residual cv1 goes to a temporary
+        y0 = plan.alloc(x.n, ho, wo, c_) if res is not None else y.cslice(0, c_)
+        self.cv1.emit(plan, x, y0)
+        self.cv2.emit(plan, y0, y.cslice(c_, c_), res=r1, res_mode=_lib.RES_ADD if res is not None else 0)
+        if res is not None:
+            plan.launch("ydbl_gate_add", r0.struct(), y0.struct(), 1.0, y.cslice(0, c_).struct(), what="ghost.res")
+        return y
+
+
+class Concat(nn.Module):
+    """U/nn/modules/conv.py:349-359 — inputs are normally already slices of the output (see tasks.py)."""
+
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+
+    def emit(self, plan, xs, out=None):
+        c = sum(x.c for x in xs)
+        y = out if out is not None else plan.alloc(xs[0].n, xs[0].h, xs[0].w, c)
+        off = 0
+        for x in xs:
+            dst = y.cslice(off, x.c)
+            if not (x.base is dst.base and x.off == dst.off and x.cs == dst.cs):
+                emit_copy(plan, x, dst)
+            off += x.c
+        return y
+
+
+# =============================================================================== block.py
+class Bottleneck(nn.Module):
+    """U/nn/modules/block.py:344-357."""
+
+    def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, k[0], 1)
+        self.cv2 = Conv(c_, c2, k[1], 1, g=g)
+        self.add = shortcut and c1 == c2
+
+    def emit(self, plan, x, out=None):
+        t = self.cv1.emit(plan, x)
+        return self.cv2.emit(plan, t, out, res=x if self.add else None,
+                             res_mode=_lib.RES_ADD if self.add else _lib.RES_NONE)
+
+
+class C2f(nn.Module):
+    """U/nn/modules/block.py:234-249."""
+
+    def __init__(self, c1, c2, n=1, shortcut=False, g=1, e=0.5):
+        super().__init__()
+        self.c = int(c2 * e)
+        self.cv1 = Conv(c1, 2 * self.c, 1, 1)
+        self.cv2 = Conv((2 + n) * self.c, c2, 1)
+        self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
+
+    def emit(self, plan, x, out=None):
+        c, n = self.c, len(self.m)
+        buf = plan.alloc(x.n, x.h, x.w, (2 + n) * c)
+        self.cv1.emit(plan, x, buf.cslice(0, 2 * c))
+        for i, m in enumerate(self.m):
+            m.emit(plan, buf.cslice((1 + i) * c, c), buf.cslice((2 + i) * c, c))
+        return self.cv2.emit(plan, buf, out)
+
+
+class C3(nn.Module):
+    """U/nn/modules/block.py:259-273."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c1, c_, 1, 1)
+        self.cv3 = Conv(2 * c_, c2, 1)
+        self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, k=((1, 1), (3, 3)), e=1.0) for _ in range(n)))
+
+    def emit(self, plan, x, out=None):
+        c_ = self.cv1.conv.out_channels
+        buf = plan.alloc(x.n, x.h, x.w, 2 * c_)
+        t = self.cv1.emit(plan, x)
+        emit_seq(plan, self.m, t, buf.cslice(0, c_))
+        self.cv2.emit(plan, x, buf.cslice(c_, c_))
+        return self.cv3.emit(plan, buf, out)
+
+
+class GhostBottleneck(nn.Module):
+    """U/nn/modules/block.py:323-341 (stride 1 on the DBL path)."""
+
+    def __init__(self, c1, c2, k=3, s=1):
+        super().__init__()
+        c_ = c2 // 2
+        self.conv = nn.Sequential(
+            GhostConv(c1, c_, 1, 1),
+            DWConv(c_, c_, k, s, act=False) if s == 2 else nn.Identity(),
+            GhostConv(c_, c2, 1, 1, act=False),
+        )
+        self.shortcut = (
+            nn.Sequential(DWConv(c1, c1, k, s, act=False), Conv(c1, c2, 1, 1, act=False)) if s == 2 else nn.Identity()
+        )
+
+    def emit(self, plan, x, out=None):
+        if not isinstance(self.shortcut, nn.Identity):
+            raise NotImplementedError("GhostBottleneck s=2 is not on the DBL path")
+        t = self.conv[0].emit(plan, x)
+        return self.conv[2].emit(plan, t, out, res=x)
+
+
+class C3Ghost(C3):
+    """U/nn/modules/block.py:313-320."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        c_ = int(c2 * e)
+        self.m = nn.Sequential(*(GhostBottleneck(c_, c_) for _ in range(n)))
+
+
+class DSBottleneck(nn.Module):
+    """U/nn/modules/block.py:1408-1444."""
+
+    def __init__(self, c1, c2, shortcut=True, e=0.5, k1=3, k2=5, d2=1):
+        super().__init__()
+        c_ = int(c2 * e)
+        self.cv1 = DSConv(c1, c_, k1, s=1, p=None, d=1)
+        self.cv2 = DSConv(c_, c2, k2, s=1, p=None, d=d2)
+        self.add = shortcut and c1 == c2
+
+    def emit(self, plan, x, out=None):
+        t = self.cv1.emit(plan, x)
+        return self.cv2.emit(plan, t, out, res=x if self.add else None,
+                             res_mode=_lib.RES_ADD if self.add else _lib.RES_NONE)
+
+
+class DSC3k(C3):
+    """U/nn/modules/block.py:1447-1503."""
+
+    def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5, k1=3, k2=5, d2=1):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        c_ = int(c2 * e)
+        self.m = nn.Sequential(
+            *(DSBottleneck(c_, c_, shortcut=shortcut, e=1.0, k1=k1, k2=k2, d2=d2) for _ in range(n))
+        )
+
+
+class DSC3k2(C2f):
+    """U/nn/modules/block.py:1505-1580."""
+
+    def __init__(self, c1, c2, n=1, dsc3k=False, e=0.5, g=1, shortcut=True, k1=3, k2=7, d2=1):
+        super().__init__(c1, c2, n, shortcut, g, e)
+        if dsc3k:
+            self.m = nn.ModuleList(
+                DSC3k(self.c, self.c, n=2, shortcut=shortcut, g=g, e=1.0, k1=k1, k2=k2, d2=d2) for _ in range(n)
+            )
+        else:
+            self.m = nn.ModuleList(
+                DSBottleneck(self.c, self.c, shortcut=shortcut, e=1.0, k1=k1, k2=k2, d2=d2) for _ in range(n)
+            )
+
+
+class AdaHyperedgeGen(nn.Module):
+    """U/nn/modules/block.py:1582-1657 (parameters only; compute in ydbl_hg_*)."""
+
+    def __init__(self, node_dim, num_hyperedges, num_heads=4, dropout=0.1, context="both"):
+        super().__init__()
+        if context != "both":
+            raise NotImplementedError("only context='both' (the DBL configuration) has a HIP path")
+        self.num_heads = num_heads
+        self.num_hyperedges = num_hyperedges
+        self.head_dim = node_dim // num_heads
+        self.context = context
+        self.prototype_base = nn.Parameter(torch.Tensor(num_hyperedges, node_dim))
+        nn.init.xavier_uniform_(self.prototype_base)
+        self.context_net = nn.Linear(2 * node_dim, num_hyperedges * node_dim)
+        self.pre_head_proj = nn.Linear(node_dim, node_dim)
+        self.dropout = nn.Dropout(dropout)
+        self.scaling = math.sqrt(self.head_dim)
+
+
+class AdaHGConv(nn.Module):
+    """U/nn/modules/block.py:1659-1708."""
+
+    def __init__(self, embed_dim, num_hyperedges=16, num_heads=4, dropout=0.1, context="both"):
+        super().__init__()
+        self.edge_generator = AdaHyperedgeGen(embed_dim, num_hyperedges, num_heads, dropout, context)
+        self.edge_proj = nn.Sequential(nn.Linear(embed_dim, embed_dim), nn.GELU())
+        self.node_proj = nn.Sequential(nn.Linear(embed_dim, embed_dim), nn.GELU())
+
+    def emit(self, plan, x, out=None):
+        g = self.edge_generator
+        D, E = x.c, g.num_hyperedges
+        y = out if out is not None else plan.alloc(x.n, x.h, x.w, D)
+        # X_proj = pre_head_proj(X) as a 1x1 conv over the token grid
+        xp = plan.alloc(x.n, x.h, x.w, D)
+        emit_dense(plan, x, xp, g.pre_head_proj.weight.detach().float().cpu().view(D, D, 1, 1),
+                   g.pre_head_proj.bias.detach().float().cpu(), what="AdaHG.pre_proj")
+        ws = plan.scratch(_lib.lib.ydbl_hg_workspace(x.n, x.h * x.w, D, E))
+        c = plan.const
+        p = [c(g.prototype_base.float()), c(g.context_net.weight.float()), c(g.context_net.bias.float()),
+             c(self.edge_proj[0].weight.float()), c(self.edge_proj[0].bias.float()),
+             c(self.node_proj[0].weight.float()), c(self.node_proj[0].bias.float())]
+        d = HgDesc(x.struct(), xp.struct(), y.struct(), E, g.num_heads, *[t.data_ptr() for t in p], ws.data_ptr())
+        plan.launch("ydbl_hg_context", d, what="AdaHG.context", keep=[d, ws, *p])
+        plan.launch("ydbl_hg_propagate", d, what="AdaHG.propagate", keep=[d])
+        return y
+
+
+class AdaHGComputation(nn.Module):
+    """U/nn/modules/block.py:1710-1752 (NHWC pixels are already the token sequence)."""
+
+    def __init__(self, embed_dim, num_hyperedges=16, num_heads=8, dropout=0.1, context="both"):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.hgnn = AdaHGConv(embed_dim, num_hyperedges, num_heads, dropout, context)
+
+    def emit(self, plan, x, out=None):
+        return self.hgnn.emit(plan, x, out)
+
+
+class C3AH(nn.Module):
+    """U/nn/modules/block.py:1754-1795."""
+
+    def __init__(self, c1, c2, e=1.0, num_hyperedges=8, context="both"):
+        super().__init__()
+        c_ = int(c2 * e)
+        assert c_ % 16 == 0, "Dimension of AdaHGComputation should be a multiple of 16."
+        self.cv1 = Conv(c1, c_, 1, 1)
+        self.cv2 = Conv(c1, c_, 1, 1)
+        self.m = AdaHGComputation(c_, num_hyperedges, c_ // 16, 0.1, context)
+        self.cv3 = Conv(2 * c_, c2, 1)
+
+    def emit(self, plan, x, out=None):
+        c_ = self.cv1.conv.out_channels
+        buf = plan.alloc(x.n, x.h, x.w, 2 * c_)
+        t = self.cv1.emit(plan, x)
+        self.m.emit(plan, t, buf.cslice(0, c_))
+        self.cv2.emit(plan, x, buf.cslice(c_, c_))
+        return self.cv3.emit(plan, buf, out)
+
+
+class FuseModule(nn.Module):
+    """U/nn/modules/block.py:1797-1840."""
+
+    def __init__(self, c_in, channel_adjust):
+        super().__init__()
+        self.downsample = nn.AvgPool2d(kernel_size=2)
+        self.upsample = nn.Upsample(scale_factor=2, mode="nearest")
+        self.conv_out = Conv((4 if channel_adjust else 3) * c_in, c_in, 1)
+
+    def emit(self, plan, xs, out=None):
+        p3, p4, p5 = xs
+        cat = plan.alloc(p4.n, p4.h, p4.w, p3.c + p4.c + p5.c)
+        plan.launch("ydbl_pool_up_concat", p3.struct(), p4.struct(), p5.struct(), cat.struct(), what="Fuse.cat")
+        return self.conv_out.emit(plan, cat, out)
+
+
+class HyperACE(nn.Module):
+    """U/nn/modules/block.py:1842-1895."""
+
+    def __init__(self, c1, c2, n=1, num_hyperedges=8, dsc3k=True, shortcut=False, e1=0.5, e2=1, context="both",
+                 channel_adjust=True):
+        super().__init__()
+        self.c = int(c2 * e1)
+        self.cv1 = Conv(c1, 3 * self.c, 1, 1)
+        self.cv2 = Conv((4 + n) * self.c, c2, 1)
+        self.m = nn.ModuleList(
+            DSC3k(self.c, self.c, 2, shortcut, k1=3, k2=7) if dsc3k else DSBottleneck(self.c, self.c, shortcut=shortcut)
+            for _ in range(n)
+        )
+        self.fuse = FuseModule(c1, channel_adjust)
+        self.branch1 = C3AH(self.c, self.c, e2, num_hyperedges, context)
+        self.branch2 = C3AH(self.c, self.c, e2, num_hyperedges, context)
+
+    def emit(self, plan, xs, out=None):
+        c, n = self.c, len(self.m)
+        x = self.fuse.emit(plan, xs)
+        # concat order of the reference: [y0, branch1(y1), y2, m_0(y2), ..., m_{n-1}, branch2(y1)]
+        cat = plan.alloc(x.n, x.h, x.w, (4 + n) * c)
+        self.cv1.emit(plan, x, cat.cslice(0, 3 * c))  # y0 | y1 | y2
+        y1 = cat.cslice(c, c)
+        self.branch2.emit(plan, y1, cat.cslice((3 + n) * c, c))
+        self.branch1.emit(plan, y1, cat.cslice(c, c))  # reads y1 before its last conv overwrites it
+        prev = cat.cslice(2 * c, c)
+        for i, m in enumerate(self.m):
+            prev = m.emit(plan, prev, cat.cslice((3 + i) * c, c))
+        return self.cv2.emit(plan, cat, out)
+
+
+class DownsampleConv(nn.Module):
+    """U/nn/modules/block.py:1897-1928."""
+
+    def __init__(self, in_channels, channel_adjust=True):
+        super().__init__()
+        self.downsample = nn.AvgPool2d(kernel_size=2)
+        self.channel_adjust = Conv(in_channels, in_channels * 2, 1) if channel_adjust else nn.Identity()
+
+    def emit(self, plan, x, out=None):
+        adjust = not isinstance(self.channel_adjust, nn.Identity)
+        pooled = out if (out is not None and not adjust) else plan.alloc(x.n, x.h // 2, x.w // 2, x.c)
+        plan.launch("ydbl_pool_up_concat", x.struct(), None, None, pooled.struct(), what="Downsample.pool")
+        return self.channel_adjust.emit(plan, pooled, out) if adjust else pooled
+
+
+class FullPAD_Tunnel(nn.Module):  # noqa: N801 (reference name)
+    """U/nn/modules/block.py:1930-1956 — x0 + gate * x1."""
+
+    def __init__(self):
+        super().__init__()
+        self.gate = nn.Parameter(torch.tensor(0.0))
+
+    def emit(self, plan, xs, out=None):
+        a, b = xs
+        y = out if out is not None else plan.alloc(a.n, a.h, a.w, a.c)
+        plan.launch("ydbl_gate_add", a.struct(), b.struct(), float(self.gate.detach().float().cpu()), y.struct(),
+                    what="FullPAD")
+        return y
+
+
+# =============================================================================== DySample / LSKblock
+class DySample(nn.Module):
+    """U/nn/modules_upsample/DySample.py:20-81 (style 'lp', scale 2, groups 4, no scope)."""
+
+    def __init__(self, in_channels, scale=2, style="lp", groups=4, dyscope=False):
+        super().__init__()
+        if style != "lp" or dyscope or scale != 2:
+            raise NotImplementedError("DySample: only style='lp', scale=2, dyscope=False has a HIP path")
+        assert in_channels >= groups and in_channels % groups == 0
+        self.scale, self.style, self.groups = scale, style, groups
+        self.offset = nn.Conv2d(in_channels, 2 * groups * scale**2, 1)
+        nn.init.normal_(self.offset.weight, 0, 0.001)
+        nn.init.constant_(self.offset.bias, 0)
+        self.register_buffer("init_pos", self._init_pos())
+
+    def _init_pos(self):
+        h = torch.arange((-self.scale + 1) / 2, (self.scale - 1) / 2 + 1) / self.scale
+        return torch.stack(torch.meshgrid([h, h], indexing="ij")).transpose(1, 2).repeat(1, self.groups, 1).reshape(
+            1, -1, 1, 1)
+
+    def emit(self, plan, x, out=None):
+        # offset = 0.25 * conv1x1(x) + init_pos  ->  folded into the conv weights/bias (0.25 is exact)
+        w = self.offset.weight.detach().float().cpu() * 0.25
+        b = self.offset.bias.detach().float().cpu() * 0.25 + self.init_pos.detach().float().cpu().view(-1)
+        off = plan.alloc(x.n, x.h, x.w, 8 * self.groups)
+        emit_conv2d(plan, self.offset, x, off, w, b, what="DySample.offset")
+        y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)
+        plan.launch("ydbl_dysample", x.struct(), off.struct(), self.groups, y.struct(), what="DySample.sample")
+        return y
+
+
+class LSKblock(nn.Module):
+    """U/nn/modules_attention/LSKA.py:28-52."""
+
+    def __init__(self, dim):
+        super().__init__()
+        self.conv0 = nn.Conv2d(dim, dim, 5, padding=2, groups=dim)
+        self.conv_spatial = nn.Conv2d(dim, dim, 7, stride=1, padding=9, groups=dim, dilation=3)
+        self.conv1 = nn.Conv2d(dim, dim // 2, 1)
+        self.conv2 = nn.Conv2d(dim, dim // 2, 1)
+        self.conv_squeeze = nn.Conv2d(2, 2, 7, padding=3)
+        self.conv = nn.Conv2d(dim // 2, dim, 1)
+
+    def emit(self, plan, x, out=None):
+        half = self.conv1.out_channels
+        a1 = emit_conv2d(plan, self.conv0, x, None, what="LSK.dw5")
+        a2 = emit_conv2d(plan, self.conv_spatial, a1, None, what="LSK.dw7d3")
+        attn = plan.alloc(x.n, x.h, x.w, 2 * half)
+        emit_conv2d(plan, self.conv1, a1, attn.cslice(0, half), what="LSK.conv1")
+        emit_conv2d(plan, self.conv2, a2, attn.cslice(half, half), what="LSK.conv2")
+        gated = plan.alloc(x.n, x.h, x.w, half)
+        ws = plan.scratch(_lib.lib.ydbl_lsk_gate_workspace(x.n, x.h, x.w))
+        sw = plan.const(self.conv_squeeze.weight.float())
+        sb = plan.const(self.conv_squeeze.bias.float())
+        plan.launch("ydbl_lsk_gate", attn.struct(), sw.data_ptr(), sb.data_ptr(), gated.struct(), ws.data_ptr(),
+                    what="LSK.gate", keep=[sw, sb, ws])
+        return emit_conv2d(plan, self.conv, gated, out, res=x, res_mode=_lib.RES_MUL, what="LSK.conv")
+
+
+# =============================================================================== head
+class DFL(nn.Module):
+    """U/nn/modules/block.py:65-84 (fixed 0..15 expectation; computed inside ydbl_detect_decode)."""
+
+    def __init__(self, c1=16):
+        super().__init__()
+        self.conv = nn.Conv2d(c1, 1, 1, bias=False).requires_grad_(False)
+        self.conv.weight.data[:] = torch.arange(c1, dtype=torch.float).view(1, c1, 1, 1)
+        self.c1 = c1
+
+
+class Detect(nn.Module):
+    """U/nn/modules/head.py:21-198 — per level cat(cv2 box branch, cv3 cls branch); decode in ydbl_detect_decode."""
+
+    dynamic = False
+    export = False
+    end2end = False
+    max_det = 300
+    shape = None
+    legacy = False
+
+    def __init__(self, nc: int = 80, ch: tuple = (), legacy: bool | None = None):
+        super().__init__()
+        self.nc = nc
+        self.nl = len(ch)
+        self.reg_max = 16
+        self.no = nc + self.reg_max * 4
+        self.stride = torch.zeros(self.nl)
+        if legacy is not None:
+            self.legacy = legacy
+        c2, c3 = max((16, ch[0] // 4, self.reg_max * 4)), max(ch[0], min(self.nc, 100))
+        self.cv2 = nn.ModuleList(
+            nn.Sequential(Conv(x, c2, 3), Conv(c2, c2, 3), nn.Conv2d(c2, 4 * self.reg_max, 1)) for x in ch
+        )
+        self.cv3 = (
+            nn.ModuleList(nn.Sequential(Conv(x, c3, 3), Conv(c3, c3, 3), nn.Conv2d(c3, self.nc, 1)) for x in ch)
+            if self.legacy
+            else nn.ModuleList(
+                nn.Sequential(
+                    nn.Sequential(DWConv(x, x, 3), Conv(x, c3, 1)),
+                    nn.Sequential(DWConv(c3, c3, 3), Conv(c3, c3, 1)),
+                    nn.Conv2d(c3, self.nc, 1),
+                )
+                for x in ch
+            )
+        )
+        self.dfl = DFL(self.reg_max)
+
+    def bias_init(self):
+        """U/nn/modules/head.py:183-194."""
+        for a, b, s in zip(self.cv2, self.cv3, self.stride):
+            a[-1].bias.data[:] = 1.0
+            b[-1].bias.data[: self.nc] = math.log(5 / self.nc / (640 / s) ** 2)
+
+    def emit(self, plan, xs, out=None):
+        """Per level: one NHWC buffer [B,h,w,64+nc] (box logits | class logits) = the reference's x[i]."""
+        levels = []
+        for i, x in enumerate(xs):
+            lv = plan.alloc(x.n, x.h, x.w, self.no)
+            t = self.cv2[i][0].emit(plan, x)
+            t = self.cv2[i][1].emit(plan, t)
+            emit_conv2d(plan, self.cv2[i][2], t, lv.cslice(0, 4 * self.reg_max), what="Detect.box")
+            if self.legacy:
+                u = self.cv3[i][0].emit(plan, x)
+                u = self.cv3[i][1].emit(plan, u)
+            else:
+                u = emit_seq(plan, self.cv3[i][0], x)
+                u = emit_seq(plan, self.cv3[i][1], u)
+            emit_conv2d(plan, self.cv3[i][2], u, lv.cslice(4 * self.reg_max, self.nc), what="Detect.cls")
+            levels.append(lv)
+        return levels
+
+
+def emit_module(m: nn.Module, plan: Plan, x, out=None):
+    """Emit any parsed layer: plugin modules or nn.Sequential repeats."""
+    if isinstance(m, nn.Sequential):
+        return emit_seq(plan, m, x, out)
+    if not hasattr(m, "emit"):
+        raise NotImplementedError(f"{type(m).__name__} has no HIP implementation")
+    return m.emit(plan, x, out)

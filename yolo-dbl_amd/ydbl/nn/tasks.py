@@ -1,0 +1,290 @@
+"""Model construction (YAML -> layers) and plan compilation for the MI355X path.
+
+Construction follows U/nn/tasks.py:947-1242 (parse_model, yaml_model_load,
+guess_model_scale) for the layer types the DBL configurations use; modules
+are looked up BY CLASS NAME, exactly like the reference's plugin mechanism
+(``globals()[m]``, U/nn/tasks.py:974), so ``register_module`` can swap in
+another implementation with the same constructor signature.
+
+``DetectionModel.compile(batch, h, w, dtype)`` turns the layer list into a
+``Plan`` (U/nn/tasks.py:145-172 ``_predict_once`` order), with every Concat
+input written in place into its slice of the concat buffer.
+"""
+
+from __future__ import annotations
+
+import json
+import math
+import re
+from copy import deepcopy
+from pathlib import Path
+
+import torch
+import torch.nn as nn
+
+from ..runtime import TV, Plan, round_up
+from . import modules as M
+
+CFG_DIR = Path(__file__).resolve().parent.parent / "cfg" / "models"
+
+# class-name registry = the reference's globals() lookup
+REGISTRY: dict[str, type] = {
+    c.__name__: c
+    for c in (M.Conv, M.DWConv, M.DSConv, M.GhostConv, M.Concat, M.Bottleneck, M.C2f, M.C3, M.C3Ghost,
+              M.GhostBottleneck, M.DSBottleneck, M.DSC3k, M.DSC3k2, M.HyperACE, M.DownsampleConv,
+              M.FullPAD_Tunnel, M.DySample, M.LSKblock, M.Detect)
+}
+_C1C2 = {"Conv", "DWConv", "GhostConv", "Bottleneck", "GhostBottleneck", "C2f", "C3", "C3Ghost", "DSC3k2", "DSConv",
+         "DSBottleneck"}
+_REPEAT_ARG = {"C2f", "C3", "C3Ghost", "DSC3k2"}
+_C1_ONLY = {"DySample", "LSKblock"}
+
+
+def register_module(cls, name: str | None = None):
+    """Plug a module class in under a YAML name (same constructor contract as the reference)."""
+    REGISTRY[name or cls.__name__] = cls
+    return cls
+
+
+def make_divisible(x, divisor):
+    """U/utils/ops.py:130-143."""
+    if isinstance(divisor, torch.Tensor):
+        divisor = int(divisor.max())
+    return math.ceil(x / divisor) * divisor
+
+
+def guess_model_scale(model_path) -> str:
+    """U/nn/tasks.py:1227-1242."""
+    m = re.search(r"yolo[v]?\d+([nslmx])", Path(model_path).stem)
+    return m.group(1) if m else ""
+
+
+def yaml_model_load(path) -> dict:
+    """U/nn/tasks.py:1211-1224: 'yolov13n_DBL.yaml' -> unified 'yolov13_DBL' config with scale 'n'.
+
+    Built-in configs live in ydbl/cfg/models/*.json; an existing .yaml/.json path is read directly.
+    """
+    path = Path(path)
+    unified = re.sub(r"(\d+)([nslmx])(.+)?$", r"\1\3", path.stem)
+    if path.exists():
+        if path.suffix in (".yaml", ".yml"):
+            import yaml
+
+            d = yaml.safe_load(path.read_text())
+        else:
+            d = json.loads(path.read_text())
+    else:
+        for cand in (CFG_DIR / f"{unified}.json", CFG_DIR / f"{path.stem}.json"):
+            if cand.exists():
+                d = json.loads(cand.read_text())
+                break
+        else:
+            raise FileNotFoundError(f"model config '{path}' not found (built-in: {sorted(p.stem for p in CFG_DIR.glob('*.json'))})")
+    d["scale"] = guess_model_scale(path)
+    d["yaml_file"] = str(path)
+    return d
+
+
+def parse_model(d: dict, ch: int = 3, verbose: bool = False):
+    """U/nn/tasks.py:947-1208 for the module set of the DBL configs."""
+    legacy = True
+    nc, scales = d.get("nc"), d.get("scales")
+    depth, width, max_channels = d.get("depth_multiple", 1.0), d.get("width_multiple", 1.0), float("inf")
+    scale = "?"
+    if scales:
+        scale = d.get("scale") or tuple(scales.keys())[0]
+        if scale not in scales:
+            raise KeyError(f"scale '{scale}' not defined by this config (available: {list(scales)})")
+        depth, width, max_channels = scales[scale]
+    ch = [ch]
+    layers, save, c2 = [], [], ch[-1]
+    for i, (f, n, name, args) in enumerate(d["backbone"] + d["head"]):
+        if name not in REGISTRY:
+            raise KeyError(f"module '{name}' (layer {i}) has no MI355X implementation")
+        m = REGISTRY[name]
+        args = [nc if a == "nc" else a for a in args]
+        n = n_ = max(round(n * depth), 1) if n > 1 else n
+        if name in _C1C2:
+            c1, c2 = ch[f], args[0]
+            if c2 != nc:
+                c2 = make_divisible(min(c2, max_channels) * width, 8)
+            args = [c1, c2, *args[1:]]
+            if name in _REPEAT_ARG:
+                args.insert(2, n)
+                n = 1
+            if name == "DSC3k2":
+                legacy = False
+        elif name == "Concat":
+            c2 = sum(ch[x] for x in f)
+        elif name == "Detect":
+            args.append([ch[x] for x in f])
+        elif name == "HyperACE":
+            legacy = False
+            c1 = ch[f[1]]
+            c2 = make_divisible(min(args[0], max_channels) * width, 8)
+            he = args[1]
+            if scale in "n":
+                he = int(args[1] * 0.5)
+            elif scale in "x":
+                he = int(args[1] * 1.5)
+            args = [c1, c2, n, he, *args[2:]]
+            n = 1
+        elif name == "DownsampleConv":
+            c1 = ch[f]
+            c2 = c1 * 2
+            args = [c1]
+        elif name == "FullPAD_Tunnel":
+            c2 = ch[f[0]]
+        elif name in _C1_ONLY:
+            c1 = c2 = ch[f]
+            args = [c1, *args[1:]]
+        else:
+            c2 = ch[f]
+        if name == "Detect":
+            m.legacy = legacy  # class attribute, as the reference sets it (U/nn/tasks.py:1111-1112)
+            m_ = m(*args)
+        else:
+            m_ = nn.Sequential(*(m(*args) for _ in range(n))) if n > 1 else m(*args)
+        m_.np = sum(x.numel() for x in m_.parameters())
+        m_.i, m_.f, m_.type = i, f, name
+        if verbose:
+            print(f"{i:>3}{str(f):>20}{n_:>3}{m_.np:10.0f}  {name:<20}{str(args):<30}")
+        save.extend(x % i for x in ([f] if isinstance(f, int) else f) if x != -1)
+        layers.append(m_)
+        if i == 0:
+            ch = []
+        ch.append(c2)
+    return nn.Sequential(*layers), sorted(save)
+
+
+class DetectionModel(nn.Module):
+    """U/nn/tasks.py:313-359 + BaseModel.fuse (:207-235)."""
+
+    def __init__(self, cfg="yolov13n_DBL.yaml", ch=3, nc=None, verbose=False):
+        super().__init__()
+        self.yaml = cfg if isinstance(cfg, dict) else yaml_model_load(cfg)
+        ch = self.yaml["ch"] = self.yaml.get("ch", ch)
+        if nc and nc != self.yaml["nc"]:
+            self.yaml["nc"] = nc
+        self.model, self.save = parse_model(deepcopy(self.yaml), ch=ch, verbose=verbose)
+        self.names = {i: f"{i}" for i in range(self.yaml["nc"])}
+        self.inplace = self.yaml.get("inplace", True)
+        self.end2end = False
+        m = self.model[-1]
+        # Stride probe by shape propagation at 256x256 (the reference runs a train-mode forward on
+        # zeros, U/nn/tasks.py:337-350; only its output shapes are used for the strides).
+        s = 256
+        levels = self.compile(1, s, s, torch.float32, device="meta").levels
+        m.stride = torch.tensor([s / lv.h for lv in levels])
+        self.stride = m.stride
+        m.bias_init()
+        for mod in self.modules():  # U/utils/torch_utils.py:410-420
+            if isinstance(mod, nn.BatchNorm2d):
+                mod.eps = 1e-3
+                mod.momentum = 0.03
+        self._fused = False
+
+    @property
+    def nc(self):
+        return self.model[-1].nc
+
+    def fuse(self, verbose=False):
+        """BN folding happens when a plan is compiled (exactly fuse_conv_and_bn's arithmetic); kept for API parity."""
+        self._fused = True
+        return self
+
+    def is_fused(self):
+        return self._fused
+
+    def compile(self, batch: int, h: int, w: int, dtype=torch.float16, device="cuda") -> "CompiledModel":
+        """Build the launch plan of one forward: input NCHW fp32 [batch,3,h,w] -> per-level head outputs."""
+        plan = Plan(torch.device(device), dtype)
+        inp = plan.alloc(batch, h, w, 8)  # RGB padded to 8 channels (16-byte vectors)
+        x_nchw = torch.empty((batch, self.yaml["ch"], h, w), dtype=torch.float32, device=plan.device)
+        plan.buffers.append(x_nchw)
+        # Concat outputs are allocated up front; their producers write straight into the slices.
+        layers = list(self.model)
+        shapes = _propagate_shapes(layers, batch, h, w, self.yaml["ch"])
+        out_hint: dict[int, TV] = {}
+        cat_buf: dict[int, TV] = {}
+        for m in layers:
+            if m.type == "Concat":
+                srcs = [m.i - 1 if j == -1 else j for j in m.f]
+                n_, h_, w_, _ = shapes[srcs[0]]
+                buf = plan.alloc(n_, h_, w_, sum(shapes[j][3] for j in srcs))
+                cat_buf[m.i] = buf
+                off = 0
+                for j in srcs:
+                    c = shapes[j][3]
+                    if j not in out_hint and layers[j].type not in ("Concat",):
+                        out_hint[j] = buf.cslice(off, c)
+                    off += c
+        y: list[TV | None] = []
+        x = inp
+        plan.launch("ydbl_input_nchw_to_nhwc", x_nchw.data_ptr(), batch, self.yaml["ch"], h, w, 1.0, inp.struct(),
+                    what="input")
+        for m in layers:
+            if m.f != -1:
+                x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+            out = cat_buf.get(m.i, out_hint.get(m.i))
+            x = M.emit_module(m, plan, x, out)
+            y.append(x)
+        return CompiledModel(plan, x_nchw, inp, x, self.model[-1])
+
+
+class CompiledModel:
+    """A compiled forward: ``input`` (NCHW fp32 staging buffer) -> ``levels`` (per-level NHWC head outputs)."""
+
+    def __init__(self, plan: Plan, x_nchw: torch.Tensor, inp: TV, levels: list[TV], detect: M.Detect):
+        self.plan, self.input, self.inp, self.levels, self.detect = plan, x_nchw, inp, levels, detect
+
+    def feats(self):
+        """Reference-layout per-level outputs x[i] = cat(box, cls) as NCHW views (no copy)."""
+        return [lv.nchw() for lv in self.levels]
+
+
+def _propagate_shapes(layers, batch, h, w, ch):
+    """Output NHWC shape of every layer (cheap symbolic pass over module types)."""
+    shapes = []
+    cur = (batch, h, w, ch)
+    for m in layers:
+        if m.f != -1:
+            src = shapes[m.f] if isinstance(m.f, int) else [cur if j == -1 else shapes[j] for j in m.f]
+        else:
+            src = cur
+        t = m.type
+        mm = m[0] if isinstance(m, nn.Sequential) else m
+        if t in ("Conv", "DWConv"):
+            k, s, p, d = mm.conv.kernel_size[0], mm.conv.stride[0], mm.conv.padding[0], mm.conv.dilation[0]
+            ho, wo = M.conv_out_hw(src[1], src[2], k, s, p, d)
+            cur = (batch, ho, wo, (m[-1] if isinstance(m, nn.Sequential) else m).conv.out_channels)
+        elif t == "DSConv":
+            k, s, p, d = mm.dw.kernel_size[0], mm.dw.stride[0], mm.dw.padding[0], mm.dw.dilation[0]
+            ho, wo = M.conv_out_hw(src[1], src[2], k, s, p, d)
+            cur = (batch, ho, wo, (m[-1] if isinstance(m, nn.Sequential) else m).pw.out_channels)
+        elif t in ("Bottleneck", "DSBottleneck"):
+            cur = (batch, src[1], src[2], (m[-1] if isinstance(m, nn.Sequential) else m).cv2.conv.out_channels
+                   if t == "Bottleneck" else (m[-1] if isinstance(m, nn.Sequential) else m).cv2.pw.out_channels)
+        elif t in ("C2f", "DSC3k2"):
+            cur = (batch, src[1], src[2], mm.cv2.conv.out_channels)
+        elif t in ("C3", "C3Ghost"):
+            cur = (batch, src[1], src[2], mm.cv3.conv.out_channels)
+        elif t == "LSKblock":
+            cur = src
+        elif t == "HyperACE":
+            cur = (batch, src[1][1], src[1][2], mm.cv2.conv.out_channels)
+        elif t == "DySample":
+            cur = (batch, 2 * src[1], 2 * src[2], src[3])
+        elif t == "DownsampleConv":
+            c = src[3] * 2 if not isinstance(mm.channel_adjust, nn.Identity) else src[3]
+            cur = (batch, src[1] // 2, src[2] // 2, c)
+        elif t == "FullPAD_Tunnel":
+            cur = src[0]
+        elif t == "Concat":
+            cur = (batch, src[0][1], src[0][2], sum(s_[3] for s_ in src))
+        elif t == "Detect":
+            cur = None
+        else:
+            raise NotImplementedError(t)
+        shapes.append(cur)
+    return shapes

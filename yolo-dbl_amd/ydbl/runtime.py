@@ -1,0 +1,163 @@
+"""Host runtime: NHWC tensor views, launch plans and hipGraph replay.
+
+A ``Plan`` is the compiled form of one (model, batch, image size, dtype)
+configuration: every activation buffer is allocated once up front (device
+memory from torch's caching allocator) and the forward is a flat list of
+C-ABI launches with prebuilt ctypes descriptors.  ``Plan.run`` walks the list
+on one HIP stream; ``GraphRunner`` captures that walk once into a hipGraph and
+replays it, so the per-forward host cost is a single graph launch.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import time
+from dataclasses import dataclass, field
+
+import torch
+
+from . import _lib
+from ._lib import View, lib
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+class TV:
+    """NHWC view into a flat device buffer: element (n,y,x,c) at base[off + ((n*H+y)*W+x)*cs + c]."""
+
+    __slots__ = ("base", "off", "n", "h", "w", "c", "cs")
+
+    def __init__(self, base: torch.Tensor, off: int, n: int, h: int, w: int, c: int, cs: int):
+        self.base, self.off, self.n, self.h, self.w, self.c, self.cs = base, off, n, h, w, c, cs
+
+    @property
+    def dtype(self):
+        return self.base.dtype
+
+    @property
+    def ptr(self) -> int:
+        return self.base.data_ptr() + self.off * self.base.element_size()
+
+    @property
+    def shape(self):
+        return (self.n, self.h, self.w, self.c)
+
+    def cslice(self, c0: int, c: int) -> "TV":
+        assert 0 <= c0 and c0 + c <= self.c, (c0, c, self.c)
+        return TV(self.base, self.off + c0, self.n, self.h, self.w, c, self.cs)
+
+    def with_hw(self, h: int, w: int) -> "TV":
+        """Reinterpret the pixel grid (same pixel count), e.g. tokens as [N,1] images."""
+        assert h * w == self.h * self.w
+        return TV(self.base, self.off, self.n, h, w, self.c, self.cs)
+
+    def struct(self) -> View:
+        return View(self.ptr, self.n, self.h, self.w, self.c, self.cs, _lib.dtype_code(self.dtype))
+
+    def torch(self) -> torch.Tensor:
+        """Strided torch view [n,h,w,c] (no copy)."""
+        return torch.as_strided(
+            self.base, (self.n, self.h, self.w, self.c), (self.h * self.w * self.cs, self.w * self.cs, self.cs, 1),
+            self.off,
+        )
+
+    def nchw(self) -> torch.Tensor:
+        return self.torch().permute(0, 3, 1, 2)
+
+
+@dataclass
+class Step:
+    fn: object
+    args: tuple
+    what: str
+    keep: list = field(default_factory=list)
+
+
+class Plan:
+    """Flat list of C-ABI launches over preallocated device buffers."""
+
+    def __init__(self, device: torch.device, dtype: torch.dtype):
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.steps: list[Step] = []
+        self.buffers: list[torch.Tensor] = []
+        self.bytes_allocated = 0
+
+    # ---------------------------------------------------------------- memory
+    def alloc(self, n: int, h: int, w: int, c: int, dtype: torch.dtype | None = None, cs: int | None = None) -> TV:
+        dtype = dtype or self.dtype
+        cs = cs or round_up(c, 8)
+        t = torch.empty(n * h * w * cs, dtype=dtype, device=self.device)
+        self.buffers.append(t)
+        self.bytes_allocated += t.numel() * t.element_size()
+        return TV(t, 0, n, h, w, c, cs)
+
+    def scratch(self, nbytes: int) -> torch.Tensor:
+        t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        self.buffers.append(t)
+        self.bytes_allocated += t.numel()
+        return t
+
+    def const(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.detach().to(self.device).contiguous()
+        self.buffers.append(t)
+        return t
+
+    # ---------------------------------------------------------------- launches
+    def launch(self, name: str, *args, what: str = "", keep=()):
+        self.steps.append(Step(getattr(lib, name), args, what or name, list(keep)))
+
+    def run(self, stream: int | None = None):
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream if stream is None else stream)
+        for st in self.steps:
+            rc = st.fn(*st.args, s)
+            if rc:
+                _lib.check(rc, st.what)
+
+    def run_timed(self):
+        """Eager walk with a HIP event pair around every launch (same stream); returns [(what, ms)]."""
+        stream = torch.cuda.current_stream(self.device)
+        s = C.c_void_p(stream.cuda_stream)
+        evs = []
+        for st in self.steps:
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            rc = st.fn(*st.args, s)
+            b.record(stream)
+            if rc:
+                _lib.check(rc, st.what)
+            evs.append((st.what, a, b))
+        torch.cuda.synchronize(self.device)
+        return [(w, a.elapsed_time(b)) for w, a, b in evs]
+
+
+class GraphRunner:
+    """Captures Plan.run into a hipGraph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it."""
+
+    def __init__(self, plan: Plan, warmup: int = 1):
+        self.plan = plan
+        side = torch.cuda.Stream(plan.device)
+        side.wait_stream(torch.cuda.current_stream(plan.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                plan.run(side.cuda_stream)
+        torch.cuda.current_stream(plan.device).wait_stream(side)
+        torch.cuda.synchronize(plan.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            plan.run()
+        torch.cuda.synchronize(plan.device)
+
+    def replay(self):
+        self.graph.replay()
+
+
+def timed(fn, *a, sync_device=None, **k):
+    t0 = time.perf_counter()
+    r = fn(*a, **k)
+    if sync_device is not None:
+        torch.cuda.synchronize(sync_device)
+    return r, time.perf_counter() - t0
