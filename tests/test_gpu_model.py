@@ -74,7 +74,7 @@ def test_model_fp32_parity(cfg, nc, size, golden_dir):
 
 def test_dbl_n_nms_consistency_fp32(golden_dir):
     """GPU NMS on the GPU's own decoded output == oracle NMS on that same tensor (bit-exact)."""
-    from oracle.ops import non_max_suppression
+    from oracle.ops import clip_boxes, non_max_suppression
     from ydbl.utils.synthetic import blob_images
 
     p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
@@ -85,6 +85,7 @@ def test_dbl_n_nms_consistency_fp32(golden_dir):
         ref = non_max_suppression(s.pred.cpu(), conf, 0.7, multi_label=multi)
         got = s.results()
         for r, g in zip(ref, got):
+            clip_boxes(r[:, :4], (256, 256))  # postprocess -> scale_boxes -> clip_boxes (predict.py:23-41)
             assert np.array_equal(g.numpy(), r.numpy())
 
 
