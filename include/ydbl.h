@@ -24,6 +24,8 @@
  *   ydbl_dwconv2d_nhwc     <- depthwise nn.Conv2d (DSConv.dw conv.py:98, DWConv conv.py:128-133,
  *                             GhostConv.cv2 conv.py:194, LSKblock.conv0/conv_spatial LSKA.py:31-32)
  *   ydbl_input_nchw_to_nhwc<- BasePredictor.preprocess engine/predictor.py:116-134 (+ LoadTensor /255)
+ *   ydbl_conv_stem         <- preprocess (predictor.py:116-134) fused with the first backbone Conv
+ *                             (conv.py:39-63 after fuse), reading the NCHW fp32 batch directly
  *   ydbl_gate_add          <- FullPAD_Tunnel.forward nn/modules/block.py:1954-1956
  *   ydbl_pool_up_concat    <- FuseModule.forward block.py:1831-1840, DownsampleConv block.py:1927
  *   ydbl_dysample          <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
@@ -89,6 +91,13 @@ int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream);
 /* NCHW fp32 image batch -> NHWC view (channels >= 3 zero-filled up to y.cs), optional scale (1/255). */
 int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,
                             const ydbl_view* y, void* stream);
+
+/* Stem: y = act(conv_kxk(x * scale) + bias) straight from an NCHW fp32 batch x [n][cin][h][w]
+ * (cin 1..3), w fp32 [cout][cin][k][k] (torch layout, BN folded), bias fp32 [cout]; y NHWC view with
+ * y.c = cout (multiple of 4, <= 64); k = 3, pad = 1, stride 1 or 2.  In f16 mode the scaled input is rounded
+ * to f16 before the conv (the reference's .half() input); arithmetic is fp32. */
+int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, float scale, const float* wt,
+                   const float* bias, int32_t k, int32_t stride, int32_t act, const ydbl_view* y, void* stream);
 
 /* y = a + gate * b (FullPAD_Tunnel). */
 int ydbl_gate_add(const ydbl_view* a, const ydbl_view* b, float gate, const ydbl_view* y, void* stream);

@@ -79,9 +79,43 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin,cout,s,h,w,res", [
+    (8, 8, 1, 70, 66, None), (8, 16, 2, 130, 140, None), (16, 8, 1, 67, 75, None), (16, 32, 2, 131, 129, "add"),
+    (32, 48, 1, 64, 90, "add"), (32, 64, 2, 140, 130, None), (16, 64, 1, 66, 70, None), (8, 36, 1, 80, 64, None),
+])
+def test_conv_tile(dtype, cin, cout, s, h, w, res):
+    """3x3 convs on maps >= 4096 output pixels with Cin in {8,16,32}: the LDS spatial-tile kernel."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin * 7 + cout + s)
+    n = 2
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, s, 1))
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+    ho, wo = ref.shape[2:]
+    assert ho * wo >= 4096
+    ybuf = plan.alloc(n, ho, wo, cout + 8)
+    yv = ybuf.cslice(4, cout) if cout % 8 else ybuf.cslice(8, cout)
+    rv, mode = None, _lib.RES_NONE
+    if res:
+        r = torch.randn(n, cout, ho, wo)
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD
+        ref = r.to(dtype).float() + ref
+    emit_dense(plan, xv, yv, wt, b, s, 1, 1, _lib.ACT_SILU, rv, mode)
+    _run(plan)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("c,k,s,d,bias,res", [(16, 3, 1, 1, False, False), (32, 3, 2, 1, True, False),
                                              (64, 7, 1, 1, False, True), (24, 5, 1, 1, True, False),
-                                             (16, 7, 1, 3, True, False)])
+                                             (16, 7, 1, 3, True, False), (16, 3, 1, 2, False, False),
+                                             (40, 5, 2, 1, True, True)])
 def test_dwconv(dtype, c, k, s, d, bias, res):
     from ydbl.nn.modules import emit_dw
 
@@ -104,6 +138,29 @@ def test_dwconv(dtype, c, k, s, d, bias, res):
     emit_dw(plan, xv, yv, wt, b, s, p, d, res=rv)
     _run(plan)
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cout,s,h,w", [(8, 1, 14, 19), (16, 2, 16, 22), (32, 1, 9, 40), (64, 2, 7, 33)])
+def test_stem(dtype, cout, s, h, w):
+    """ydbl_conv_stem (preprocess + first Conv) vs conv2d on the dtype-rounded image."""
+    from ydbl import _lib
+
+    torch.manual_seed(cout + s)
+    n = 3
+    x = torch.rand(n, 3, h, w)
+    wt = torch.randn(cout, 3, 3, 3) / 27 ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt, b, s, 1))
+    plan = _plan(dtype)
+    ho, wo = ref.shape[2:]
+    yv = plan.alloc(n, ho, wo, cout)
+    xd, wd, bd = x.to(DEV), wt.to(DEV), b.to(DEV)
+    plan.launch("ydbl_conv_stem", xd.data_ptr(), n, 3, h, w, 1.0, wd.data_ptr(), bd.data_ptr(), 3, s,
+                _lib.ACT_SILU, yv.struct())
+    _run(plan)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
 
 
 def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False):
@@ -284,6 +341,9 @@ def _rand_pred(n, nc, A, seed, ties=False):
     dict(nc=3, A=5000, conf=0.01, iou=0.7, multi=True, max_det=50),
     dict(nc=3, A=6000, conf=0.01, iou=0.9, multi=True, max_nms=3000),
     dict(nc=3, A=100, conf=0.999, iou=0.7, multi=False),  # (almost) empty
+    dict(nc=2, A=4000, conf=0.05, iou=0.6, multi=True),  # 4096 < n <= 8192: LDS sort, global box reads
+    dict(nc=1, A=64, conf=0.0, iou=0.0, multi=False),  # iou 0: every overlap suppresses
+    dict(nc=3, A=3000, conf=0.2, iou=0.7, multi=False, max_det=1),
 ])
 def test_nms_bit_exact(case):
     from oracle.ops import non_max_suppression as ref_nms

@@ -40,89 +40,134 @@ __device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& 
   return c;
 }
 
-// POINTWISE: 1x1, stride 1, pad 0 (x is a dense [P][xcs] matrix).
-template <typename T, int MT, int NT, bool POINTWISE>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs<T> p) {
+// LDS-staged implicit GEMM.  Workgroup tile = BM output pixels x BN output channels, 4 waves as
+// WM x WN, each wave TM x TN MFMA tiles of 16x16.  K (= taps x Cin, tap-major, NHWC-contiguous
+// within a tap) advances in steps of BK = four 16-byte vectors per row (32 f16 / 16 f32):
+//   global -> registers (step s+1, issued before the MFMAs of step s) -> LDS (double buffer)
+//   -> fragments (ds_read_b128, XOR-swizzled rows: conflict-free for the 16x16 fragment pattern)
+// A = weights [cout][KPAD] (rows shared by the WM waves of a column), B = im2col rows gathered
+// on the fly (shared by the WN waves of a row); one barrier per k-step.
+template <int R>
+__device__ __forceinline__ int swz(int row, int kv) {  // 16B-slot swizzle within a 64-byte row
+  return row * 4 + (kv ^ (((row >> 2) & 1) << 1));
+}
+
+template <typename T, int BM, int BN, int WM, int WN, bool POINTWISE>
+__global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   constexpr int VEC = Vec<T>::N;
-  constexpr int KCH = 4 * VEC;
+  constexpr int BK = 4 * VEC;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile config");
+  constexpr int A_IT = (BN * 4 + 255) / 256, B_IT = (BM * 4 + 255) / 256;
   using vec = typename Vec<T>::type;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int g = lane >> 4;
-  const int r16 = lane & 15;
-  const int px0 = (blockIdx.x * 4 + wave) * (MT * 16);
-  const int co0 = blockIdx.y * (NT * 16);
+  __shared__ vec sA[2][BN * 4];
+  __shared__ vec sB[2][BM * 4];
 
-  // Per pixel-tile B-operand coordinates for this lane.
-  int pb[MT], piy[MT], pix[MT];
-  bool pv[MT];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int wm = wave % WM, wn = wave / WM;
+  const int m0 = blockIdx.x * BM;
+  const int n0 = blockIdx.y * BN;
+
+  // ---- per-thread staging coordinates (vector v = tid + it*256: row v>>2, k-vector v&3)
+  const T* arow[A_IT];
+  bool aval[A_IT];
 #pragma unroll
-  for (int j = 0; j < MT; ++j) {
-    int pp = px0 + 16 * j + r16;
-    pv[j] = pp < p.P;
-    pp = pv[j] ? pp : 0;
-    int ox = pp % p.Wo;
-    int t = pp / p.Wo;
-    int oy = t % p.Ho;
-    pb[j] = t / p.Ho;
-    piy[j] = oy * p.S - p.PAD;
-    pix[j] = ox * p.S - p.PAD;
+  for (int it = 0; it < A_IT; ++it) {
+    const int v = tid + it * 256;
+    const int co = n0 + (v >> 2);
+    aval[it] = v < BN * 4 && co < p.Cout;
+    arow[it] = p.w + (int64_t)(aval[it] ? co : 0) * p.KPAD + (v & 3) * VEC;
   }
-  const T* wrow[NT];
-  bool wv[NT];
+  int bb[B_IT], biy[B_IT], bix[B_IT];
+  int64_t bpix[B_IT];
+  bool bval[B_IT];
 #pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    int co = co0 + 16 * i + r16;
-    wv[i] = co < p.Cout;
-    wrow[i] = p.w + (int64_t)(wv[i] ? co : 0) * p.KPAD;
+  for (int it = 0; it < B_IT; ++it) {
+    const int v = tid + it * 256;
+    int pp = m0 + (v >> 2);
+    bval[it] = v < BM * 4 && pp < p.P;
+    pp = bval[it] ? pp : 0;
+    bpix[it] = pp;
+    const int ox = pp % p.Wo;
+    const int t = pp / p.Wo;
+    const int oy = t % p.Ho;
+    bb[it] = t / p.Ho;
+    biy[it] = oy * p.S - p.PAD;
+    bix[it] = ox * p.S - p.PAD;
   }
-
-  f32x4 acc[NT][MT];
+  vec ra[A_IT], rb[B_IT];
+  auto load_step = [&](int ks) {
 #pragma unroll
-  for (int i = 0; i < NT; ++i)
+    for (int it = 0; it < A_IT; ++it) ra[it] = aval[it] ? vload(arow[it] + ks * BK) : vzero<T>();
 #pragma unroll
-    for (int j = 0; j < MT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  for (int k0 = 0; k0 < p.K; k0 += KCH) {
-    const int k = k0 + g * VEC;
-    const bool kv = k < p.K;
-    vec a[NT];
-#pragma unroll
-    for (int i = 0; i < NT; ++i) a[i] = wv[i] ? vload(wrow[i] + k) : vzero<T>();
-    vec b[MT];
-    if constexpr (POINTWISE) {
-#pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int64_t pp = px0 + 16 * j + r16;
-        b[j] = (pv[j] && kv) ? vload(p.x + pp * p.xcs + k) : vzero<T>();
+    for (int it = 0; it < B_IT; ++it) {
+      const int v = tid + it * 256;
+      const int k = ks * BK + (v & 3) * VEC;
+      vec val = vzero<T>();
+      if (bval[it] && k < p.K) {
+        if constexpr (POINTWISE) {
+          val = vload(p.x + bpix[it] * p.xcs + k);
+        } else {
+          const int tap = k / p.Cin;
+          const int ci = k - tap * p.Cin;
+          const int ky = tap / p.KW, kx = tap - ky * p.KW;
+          const int iy = biy[it] + ky * p.DIL, ix = bix[it] + kx * p.DIL;
+          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+            val = vload(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + ci);
+        }
       }
-    } else {
-      const int tap = k / p.Cin;
-      const int ci = k - tap * p.Cin;
-      const int ky = tap / p.KW;
-      const int kx = tap - ky * p.KW;
-      const int dy = ky * p.DIL, dx = kx * p.DIL;
+      rb[it] = val;
+    }
+  };
+  auto store_step = [&](int buf) {
 #pragma unroll
-      for (int j = 0; j < MT; ++j) {
-        const int iy = piy[j] + dy, ix = pix[j] + dx;
-        const bool ok = pv[j] && kv && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        b[j] = ok ? vload(p.x + ((int64_t)(pb[j] * p.H + iy) * p.W + ix) * p.xcs + ci) : vzero<T>();
-      }
+    for (int it = 0; it < A_IT; ++it) {
+      const int v = tid + it * 256;
+      if (v < BN * 4) sA[buf][swz<0>(v >> 2, v & 3)] = ra[it];
     }
 #pragma unroll
-    for (int i = 0; i < NT; ++i)
+    for (int it = 0; it < B_IT; ++it) {
+      const int v = tid + it * 256;
+      if (v < BM * 4) sB[buf][swz<0>(v >> 2, v & 3)] = rb[it];
+    }
+  };
+
+  f32x4 acc[TN][TM];
 #pragma unroll
-      for (int j = 0; j < MT; ++j) acc[i][j] = mfma_chunk<T>(a[i], b[j], acc[i][j]);
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (p.K + BK - 1) / BK;
+  load_step(0);
+  store_step(0);
+  __syncthreads();
+  for (int ks = 0; ks < nsteps; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nsteps) load_step(ks + 1);
+    vec af[TN], bf[TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) af[i] = sA[buf][swz<0>(wn * TN * 16 + i * 16 + r16, g)];
+#pragma unroll
+    for (int j = 0; j < TM; ++j) bf[j] = sB[buf][swz<0>(wm * TM * 16 + j * 16 + r16, g)];
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+    if (ks + 1 < nsteps) store_step(buf ^ 1);
+    __syncthreads();
   }
 
-  // Epilogue: lane owns channels co..co+3 of pixel px0+16j+r16.
+  // ---- epilogue: lane owns channels co..co+3 of pixel pp
 #pragma unroll
-  for (int j = 0; j < MT; ++j) {
-    if (!pv[j]) continue;
-    const int64_t pp = px0 + 16 * j + r16;
+  for (int j = 0; j < TM; ++j) {
+    const int64_t pp = m0 + wm * TM * 16 + j * 16 + r16;
+    if (pp >= p.P) continue;
 #pragma unroll
-    for (int i = 0; i < NT; ++i) {
-      const int co = co0 + 16 * i + 4 * g;
+    for (int i = 0; i < TN; ++i) {
+      const int co = n0 + wn * TN * 16 + i * 16 + 4 * g;
       if (co >= p.Cout) continue;
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       const bool full = co + 4 <= p.Cout;
@@ -154,33 +199,209 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs<T> p) {
   }
 }
 
-template <typename T, int MT, int NT>
-static void launch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(a.P, 4 * MT * 16), (unsigned)cdiv(a.Cout, NT * 16));
+// Spatial-tile 3x3 conv for thin inputs (Cin <= 32, the high-resolution backbone layers).
+// A workgroup owns a TH x TW output tile of one image and ALL output channels (NTN x 16 <= 64):
+// the input halo tile (IH x IW pixels x Cin) and the whole weight matrix [Cout][KPAD] are staged
+// in LDS once, so each input element leaves HBM/L2 about once instead of once per tap (the 9x
+// im2col amplification of conv_igemm_kernel).  B fragments are gathered from the LDS tile:
+// lane (pixel r16, k-vector g) reads the 8 channels of tap k/Cin at (py*S+ky, px*S+kx).
+// Channel-vector slots are XOR-swizzled by pixel so 16 consecutive pixels hit distinct banks.
+template <int CV>
+__device__ __forceinline__ int tswz(int pix, int cv) {
+  if constexpr (CV == 1) return pix;
+  else return pix * CV + (cv ^ ((pix / (16 / CV)) & (CV - 1)));
+}
+
+template <typename T, int CIN, int S, int TH, int TW, int NTN>
+__global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int tiles_x, int tiles_y) {
+  constexpr int VEC = Vec<T>::N;
+  constexpr int CV = CIN / VEC;                 // 16-byte channel vectors per pixel
+  constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
+  constexpr int K = 9 * CIN;
+  constexpr int BK = 4 * VEC;
+  constexpr int KPAD = (K + 31) / 32 * 32;
+  constexpr int NSTEP = (K + BK - 1) / BK;
+  constexpr int WROW = KPAD / VEC + 1;          // weight row in 16B vectors (+1 pad: bank spread)
+  constexpr int TM = TH * TW / 64;              // 16-pixel tiles per wave
+  using vec = typename Vec<T>::type;
+  __shared__ vec sx[IH * IW * CV];
+  __shared__ vec sw[NTN * 16 * WROW];
+
+  const int tid = threadIdx.x;
+  int bid = blockIdx.x;
+  const int tx = bid % tiles_x; bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - p.PAD, ix0 = ox0 * S - p.PAD;
+  {  // stage the input tile (loads batched 4 deep before their LDS stores)
+    constexpr int TOT = IH * IW * CV;
+    for (int base = 0; base < TOT; base += 4 * 256) {
+      vec t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * 256 + tid;
+        const int pix = i / CV, cv = i - pix * CV;
+        const int iy = iy0 + pix / IW, ix = ix0 + pix % IW;
+        t[u] = (i < TOT && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+                   ? vload(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + cv * VEC)
+                   : vzero<T>();
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * 256 + tid;
+        if (i < TOT) sx[tswz<CV>(i / CV, i % CV)] = t[u];
+      }
+    }
+    constexpr int WTOT = NTN * 16 * (KPAD / VEC);
+    for (int base = 0; base < WTOT; base += 4 * 256) {
+      vec t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * 256 + tid;
+        const int co = i / (KPAD / VEC), kv = i % (KPAD / VEC);
+        t[u] = (i < WTOT && co < p.Cout) ? vload(p.w + (int64_t)co * p.KPAD + kv * VEC) : vzero<T>();
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = base + u * 256 + tid;
+        if (i < WTOT) sw[(i / (KPAD / VEC)) * WROW + i % (KPAD / VEC)] = t[u];
+      }
+    }
+  }
+  __syncthreads();
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  int lbase[TM];  // LDS pixel index of each 16-pixel tile's top-left tap for this lane
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int op = wave * TM * 16 + j * 16 + r16;
+    const int py = op / TW, px = op % TW;
+    lbase[j] = (py * S) * IW + px * S;
+  }
+  f32x4 acc[NTN][TM];
+#pragma unroll
+  for (int i = 0; i < NTN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NSTEP; ++ks) {
+    const int k = ks * BK + g * VEC;
+    const bool kin = k < K;
+    const int tap = kin ? k / CIN : 0, cv = kin ? (k % CIN) / VEC : 0;
+    const int ky = tap / 3, kx = tap % 3;
+    const int toff = ky * IW + kx;
+    vec af[NTN], bf[TM];
+#pragma unroll
+    for (int i = 0; i < NTN; ++i) af[i] = sw[(i * 16 + r16) * WROW + ks * 4 + g];  // zero beyond K
+#pragma unroll
+    for (int j = 0; j < TM; ++j) bf[j] = sx[tswz<CV>(lbase[j] + toff, cv)];
+#pragma unroll
+    for (int i = 0; i < NTN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+  }
+
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int op = wave * TM * 16 + j * 16 + r16;
+    const int oy = oy0 + op / TW, ox = ox0 + op % TW;
+    if (oy >= p.Ho || ox >= p.Wo) continue;
+    const int64_t pp = ((int64_t)b * p.Ho + oy) * p.Wo + ox;
+#pragma unroll
+    for (int i = 0; i < NTN; ++i) {
+      const int co = i * 16 + 4 * g;
+      if (co >= p.Cout) continue;
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      if (p.bias) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] += p.bias[co + q];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act);
+      if (p.res != YDBL_RES_NONE) {
+        float rv[4];
+        load_f<4>(p.r + pp * p.rcs + co, rv);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (p.res == YDBL_RES_ADD) ? rv[q] + v[q] : rv[q] * v[q];
+      }
+      store_f<4>(p.y + pp * p.ycs + co, v);
+    }
+  }
+}
+
+template <typename T, int CIN, int S, int TH, int TW, int NTN>
+static void launch_tile(const ConvArgs<T>& a, hipStream_t s) {
+  const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
+  conv3x3_tile_kernel<T, CIN, S, TH, TW, NTN><<<(unsigned)(a.N * tiles_y * tiles_x), 256, 0, s>>>(a, tiles_x, tiles_y);
+}
+
+// 3x3 / pad 1 / dil 1, Cin in {8,16,32}, Cout <= 64 and a multiple of 4: the spatial-tile kernel.
+template <typename T, int CIN, int NTN>
+static void launch_tile_s(const ConvArgs<T>& a, hipStream_t s) {
+  if (a.S == 1) launch_tile<T, CIN, 1, 8, 32, NTN>(a, s);
+  else launch_tile<T, CIN, 2, 8, 16, NTN>(a, s);
+}
+
+template <typename T, int CIN>
+static bool tile_ntn(const ConvArgs<T>& a, hipStream_t s) {
+  switch ((a.Cout + 15) / 16) {
+    case 1: launch_tile_s<T, CIN, 1>(a, s); return true;
+    case 2: launch_tile_s<T, CIN, 2>(a, s); return true;
+    case 3: launch_tile_s<T, CIN, 3>(a, s); return true;
+    case 4: launch_tile_s<T, CIN, 4>(a, s); return true;
+    default: return false;
+  }
+}
+
+template <typename T>
+static bool try_tile(const ConvArgs<T>& a, int kh, hipStream_t s) {
+  if (kh != 3 || a.KW != 3 || a.DIL != 1 || a.PAD != 1 || a.Cout > 64 || a.Cout % 4) return false;
+  if (a.S != 1 && a.S != 2) return false;
+  if ((int64_t)a.Ho * a.Wo < 4096) return false;  // small maps: the GEMM kernel has more parallelism
+  if (a.xcs % Vec<T>::N) return false;
+  switch (a.Cin) {
+    case 8: return tile_ntn<T, 8>(a, s);
+    case 16: return tile_ntn<T, 16>(a, s);
+    case 32: return tile_ntn<T, 32>(a, s);
+    default: return false;
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+static void launch_igemm(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
   if (pointwise)
-    conv_mfma_kernel<T, MT, NT, true><<<grid, 256, 0, s>>>(a);
+    conv_igemm_kernel<T, BM, BN, WM, WN, true><<<grid, 256, 0, s>>>(a);
   else
-    conv_mfma_kernel<T, MT, NT, false><<<grid, 256, 0, s>>>(a);
+    conv_igemm_kernel<T, BM, BN, WM, WN, false><<<grid, 256, 0, s>>>(a);
 }
 
 template <typename T>
 static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
-  // Tile choice: cover Cout with 1/2/4 16-row tiles per wave; shrink the pixel tile until the
-  // grid has enough workgroups to fill 256 CUs.
-  const int nt = a.Cout <= 16 ? 1 : (a.Cout <= 32 ? 2 : 4);
-  auto blocks = [&](int mt) { return cdiv(a.P, 4 * mt * 16) * cdiv(a.Cout, nt * 16); };
-  if (nt == 1) {
-    if (blocks(8) >= 1024) return launch_conv<T, 8, 1>(a, pointwise, s);
-    if (blocks(4) >= 512) return launch_conv<T, 4, 1>(a, pointwise, s);
-    return launch_conv<T, 2, 1>(a, pointwise, s);
+  // BN covers Cout in one column of workgroups where it can (the input tile is then read once);
+  // BM is the largest pixel tile that still gives >= 1024 workgroups (4 per CU) to fill the chip.
+  const int64_t want = 1024;
+  auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
+  if (a.Cout <= 16) {
+    if (blocks(256, 16) >= want) return launch_igemm<T, 256, 16, 4, 1>(a, pointwise, s);
+    if (blocks(128, 16) >= want) return launch_igemm<T, 128, 16, 4, 1>(a, pointwise, s);
+    return launch_igemm<T, 64, 16, 4, 1>(a, pointwise, s);
   }
-  if (nt == 2) {
-    if (blocks(4) >= 512) return launch_conv<T, 4, 2>(a, pointwise, s);
-    return launch_conv<T, 2, 2>(a, pointwise, s);
+  if (a.Cout <= 32) {
+    if (blocks(256, 32) >= want) return launch_igemm<T, 256, 32, 4, 1>(a, pointwise, s);
+    if (blocks(128, 32) >= want) return launch_igemm<T, 128, 32, 4, 1>(a, pointwise, s);
+    return launch_igemm<T, 64, 32, 4, 1>(a, pointwise, s);
   }
-  if (blocks(4) >= 512) return launch_conv<T, 4, 4>(a, pointwise, s);
-  if (blocks(2) >= 512) return launch_conv<T, 2, 4>(a, pointwise, s);
-  return launch_conv<T, 1, 4>(a, pointwise, s);
+  if (a.Cout <= 64) {
+    if (blocks(128, 64) >= want) return launch_igemm<T, 128, 64, 2, 2>(a, pointwise, s);
+    if (blocks(64, 64) >= want) return launch_igemm<T, 64, 64, 2, 2>(a, pointwise, s);
+    return launch_igemm<T, 32, 64, 2, 2>(a, pointwise, s);
+  }
+  if (blocks(128, 128) >= want) return launch_igemm<T, 128, 128, 2, 2>(a, pointwise, s);
+  if (blocks(64, 128) >= want) return launch_igemm<T, 64, 128, 2, 2>(a, pointwise, s);
+  return launch_igemm<T, 32, 128, 2, 2>(a, pointwise, s);
 }
 
 template <typename T>
@@ -197,7 +418,7 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   a.act = d->act; a.res = d->res_mode;
   a.P = d->y.n * d->y.h * d->y.w;
   const bool pw = d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->x.h == d->y.h && d->x.w == d->y.w;
-  dispatch_conv<T>(a, pw, s);
+  if (!try_tile<T>(a, d->kh, s)) dispatch_conv<T>(a, pw, s);
   return check_launch("ydbl_conv2d_nhwc");
 }
 

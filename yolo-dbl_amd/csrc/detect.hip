@@ -147,160 +147,205 @@ __global__ __launch_bounds__(256) void pred_cand_kernel(ydbl_pred_cand_desc p) {
   }
 }
 
-// ------------------------------------------------------------------------------------ sort
-constexpr int SORT_CHUNK = 4096;
+// ------------------------------------------------------------------------------------ NMS
+// One 1024-thread workgroup per image does the whole post-filter path of U/utils/ops.py:278-310:
+//   1. sort the image's candidates by (score desc, original index asc) -- torchvision's stable
+//      descending sort over candidates that are in anchor (or torch.where) order -- bitonic in LDS
+//      for n <= NMS_SORT_LDS, in the global workspace (same workgroup, barrier-separated) above;
+//   2. truncate to max_nms (the reference's argsort(descending)[:max_nms] gives the same prefix);
+//   3. greedy sweep in chunks of 64 sorted boxes: the 16 waves compute the chunk's 64x64 upper-
+//      triangular suppression mask in parallel, wave 0 resolves the chunk serially on a wave-
+//      uniform 64-bit live mask (find-first-set, readlane of the kept row's mask, and-not), then
+//      all waves suppress every later box against the chunk's kept boxes (LDS byte flags).
+//      Kept boxes come out in score order, so stopping at max_det == keep[:max_det].
+//   IoU arithmetic is torchvision's CPU kernel in fp32: inter / (area_i + area_j - inter),
+//   compared as double against iou_thres; areas without +1; boxes offset by cls * max_wh.
+constexpr int NMS_SORT_LDS = 8192;   // candidates sorted in LDS (8 B key + 4 B slot each)
+constexpr int NMS_MAX_FLAGS = 32768;  // max_nms limit (LDS suppression flags, 1 B each)
+constexpr int NMS_MAX_DET = 4096;
+constexpr int NMS_THREADS = 1024;
 
 __device__ __forceinline__ uint64_t make_key(float score, int idx) {
-  // scores are sigmoid outputs in (0,1): their bit patterns order like the values.
+  // candidate scores are > conf_thres >= 0: positive floats order like their bit patterns.
   const uint32_t sb = __float_as_uint(score);
   return ((uint64_t)(0xFFFFFFFFu - sb) << 32) | (uint32_t)idx;
 }
 
-__global__ __launch_bounds__(1024) void nms_keys_kernel(const float* __restrict__ score, const int* __restrict__ idx,
-                                                        const int* __restrict__ count, int cap, int L,
-                                                        uint64_t* __restrict__ keys, int* __restrict__ vals) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= L) return;
-  const int n = min(count[b], cap);
-  const int64_t o = (int64_t)b * L + i;
-  if (i < n) {
-    keys[o] = make_key(score[(int64_t)b * cap + i], idx[(int64_t)b * cap + i]);
-    vals[o] = i;
-  } else {
-    keys[o] = ~0ull;
-    vals[o] = -1;
-  }
-}
-
-// Bitonic steps (k, j) for j < SORT_CHUNK inside LDS.  If full, runs every k <= chunk.
-__global__ __launch_bounds__(1024) void bitonic_local_kernel(uint64_t* __restrict__ keys, int* __restrict__ vals, int L,
-                                                             int chunk, int kfixed) {
-  __shared__ uint64_t sk[SORT_CHUNK];
-  __shared__ int sv[SORT_CHUNK];
-  const int b = blockIdx.y;
-  const int64_t base = (int64_t)b * L + (int64_t)blockIdx.x * chunk;
-  for (int i = threadIdx.x; i < chunk; i += blockDim.x) {
-    sk[i] = keys[base + i];
-    sv[i] = vals[base + i];
-  }
-  __syncthreads();
-  const int gbase = blockIdx.x * chunk;
-  auto step = [&](int k, int j) {
-    for (int t = threadIdx.x; t < chunk / 2; t += blockDim.x) {
-      const int i = 2 * j * (t / j) + (t % j);
-      const int ixj = i + j;
-      const bool up = ((gbase + i) & k) == 0;
-      const uint64_t a = sk[i], c = sk[ixj];
-      if ((a > c) == up) {
-        sk[i] = c; sk[ixj] = a;
-        const int tv = sv[i]; sv[i] = sv[ixj]; sv[ixj] = tv;
-      }
-    }
-    __syncthreads();
-  };
-  if (kfixed == 0) {
-    for (int k = 2; k <= chunk; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) step(k, j);
-  } else {
-    for (int j = chunk >> 1; j > 0; j >>= 1) step(kfixed, j);
-  }
-  for (int i = threadIdx.x; i < chunk; i += blockDim.x) {
-    keys[base + i] = sk[i];
-    vals[base + i] = sv[i];
-  }
-}
-
-__global__ __launch_bounds__(256) void bitonic_global_kernel(uint64_t* __restrict__ keys, int* __restrict__ vals, int L,
-                                                             int k, int j) {
-  const int b = blockIdx.y;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= L / 2) return;
-  const int i = 2 * j * (t / j) + (t % j);
-  const int ixj = i + j;
-  const bool up = (i & k) == 0;
-  uint64_t* kb = keys + (int64_t)b * L;
-  int* vb = vals + (int64_t)b * L;
-  const uint64_t a = kb[i], c = kb[ixj];
-  if ((a > c) == up) {
-    kb[i] = c; kb[ixj] = a;
-    const int tv = vb[i]; vb[i] = vb[ixj]; vb[ixj] = tv;
-  }
-}
-
-// ------------------------------------------------------------------------------------ greedy
-constexpr int NMS_LDS_BOXES = 4096;
-constexpr int NMS_MAX_FLAGS = 32768;
-constexpr int NMS_MAX_DET = 4096;
-
 struct NmsArgs {
-  const float* cbox; const float* cscore; const int* ccls; const int* ccount;
-  const int* vals; int L, cap;
+  const float* cbox; const float* cscore; const int* ccls; const int* cidx; const int* ccount;
+  uint64_t* gkeys; int* gvals; int L;  // global sort scratch (only when cap > NMS_SORT_LDS)
+  int cap;
   double thr; int max_det, max_nms; float off_scale;
   float clip_w, clip_h;
   float* out; int* out_count;
 };
 
-__global__ __launch_bounds__(1024) void nms_greedy_kernel(NmsArgs p) {
-  __shared__ f32x4 sbox[NMS_LDS_BOXES];
+// bitonic sort of P (power of two) key/value pairs; keys/vals in LDS or global, one workgroup
+template <typename KP, typename VP>
+__device__ void block_bitonic(KP keys, VP vals, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < P / 2; t += NMS_THREADS) {
+        const int i = 2 * j * (t / j) + (t % j);
+        const int ixj = i + j;
+        const bool up = (i & k) == 0;
+        const uint64_t a = keys[i], c = keys[ixj];
+        if ((a > c) == up) {
+          keys[i] = c; keys[ixj] = a;
+          const int tv = vals[i]; vals[i] = vals[ixj]; vals[ixj] = tv;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4& b, double thr) {
+  const float xx1 = fmaxf(a[0], b[0]), yy1 = fmaxf(a[1], b[1]);
+  const float xx2 = fminf(a[2], b[2]), yy2 = fminf(a[3], b[3]);
+  const float ww = fmaxf(0.f, xx2 - xx1), hh = fmaxf(0.f, yy2 - yy1);
+  const float inter = ww * hh;
+  const float area_b = (b[2] - b[0]) * (b[3] - b[1]);
+  const float ovr = inter / ((area_a + area_b) - inter);
+  return (double)ovr > thr;
+}
+
+__global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
+  // LDS: sort keys (64 KB) are reused for the first 4096 sorted boxes after sorting.
+  __shared__ uint64_t s_keys[NMS_SORT_LDS];
+  __shared__ int s_vals[NMS_SORT_LDS];
   __shared__ unsigned char removed[NMS_MAX_FLAGS];
-  __shared__ int kept_slot[NMS_MAX_DET];
-  __shared__ int s_next;
+  __shared__ int kept_sorted[NMS_MAX_DET];
+  __shared__ f32x4 chunk_box[64];
+  __shared__ unsigned char cmask[64][16];
+  __shared__ int s_nk;
+  f32x4* s_box = reinterpret_cast<f32x4*>(s_keys);
+  constexpr int LDS_BOXES = NMS_SORT_LDS * 8 / 16;
+
   const int b = blockIdx.x;
-  const int n = min(min(p.ccount[b], p.cap), p.max_nms);
-  const int* vb = p.vals + (int64_t)b * p.L;
+  const int n = min(p.ccount[b], p.cap);
+  const float* sc = p.cscore + (int64_t)b * p.cap;
+  const int* ix = p.cidx + (int64_t)b * p.cap;
+  // ---- 1. sort
+  const bool in_lds = n <= NMS_SORT_LDS;
+  int P = 64;
+  while (P < n) P <<= 1;
+  const int* order;  // sorted position -> candidate slot
+  if (in_lds) {
+    for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
+      s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+      s_vals[i] = i < n ? i : -1;
+    }
+    __syncthreads();
+    if (n > 1) block_bitonic(s_keys, s_vals, P);
+    order = s_vals;
+  } else {
+    uint64_t* gk = p.gkeys + (int64_t)b * p.L;
+    int* gv = p.gvals + (int64_t)b * p.L;
+    for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
+      gk[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+      gv[i] = i < n ? i : -1;
+    }
+    __syncthreads();
+    block_bitonic(gk, gv, P);
+    order = gv;
+  }
+  const int m = min(n, p.max_nms);
+  // ---- stage boxes (class-offset) of the first LDS_BOXES sorted candidates; flags
+  const float* cb = p.cbox + (int64_t)b * p.cap * 4;
+  const int* cc = p.ccls + (int64_t)b * p.cap;
   auto load_box = [&](int i) -> f32x4 {
-    const int slot = vb[i];
-    const int64_t o = (int64_t)b * p.cap + slot;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(p.cbox + o * 4);
-    const float c = float(p.ccls[o]) * p.off_scale;  // boxes + cls * max_wh (0 if agnostic)
+    const int slot = order[i];
+    const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)slot * 4);
+    const float c = float(cc[slot]) * p.off_scale;  // boxes + cls * max_wh (0 if agnostic)
     return f32x4{v[0] + c, v[1] + c, v[2] + c, v[3] + c};
   };
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    removed[i] = 0;
-    if (i < NMS_LDS_BOXES) sbox[i] = load_box(i);
+  // s_box aliases s_keys: read every box first, then write (order[] = s_vals is separate)
+  f32x4 mine[LDS_BOXES / NMS_THREADS];
+#pragma unroll
+  for (int r = 0; r < LDS_BOXES / NMS_THREADS; ++r) {
+    const int i = threadIdx.x + r * NMS_THREADS;
+    if (i < m) mine[r] = load_box(i);
   }
   __syncthreads();
-  int kept = 0, cur = 0;
+#pragma unroll
+  for (int r = 0; r < LDS_BOXES / NMS_THREADS; ++r) {
+    const int i = threadIdx.x + r * NMS_THREADS;
+    if (i < m) s_box[i] = mine[r];
+  }
+  for (int i = threadIdx.x; i < m; i += NMS_THREADS) removed[i] = 0;
+  if (threadIdx.x == 0) s_nk = 0;
+  __syncthreads();
+  auto box_at = [&](int i) -> f32x4 { return i < LDS_BOXES ? s_box[i] : load_box(i); };
+
+  // ---- 3. chunked greedy sweep
   const int lane = threadIdx.x & 63;
-  while (true) {
-    if (threadIdx.x < 64) {  // wave 0: first non-removed index >= cur
-      int found = n;
-      for (int base = cur; base < n; base += 64) {
-        const int i = base + lane;
-        const bool live = i < n && !removed[i];
-        const uint64_t mask = __ballot(live);
-        if (mask) {
-          found = base + __ffsll((long long)mask) - 1;
+  const int wave = threadIdx.x >> 6;  // 16 waves
+  for (int c0 = 0; c0 < m; c0 += 64) {
+    const int nk0 = s_nk;
+    if (nk0 >= p.max_det) break;
+    // (a) intra-chunk suppression masks: wave w tests columns c0+4w..c0+4w+3 against row c0+lane
+    {
+      const int i = c0 + lane;
+      unsigned bits = 0;
+      if (i < m && !removed[i]) {
+        const f32x4 bi = box_at(i);
+        const float ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = c0 + 4 * wave + q;
+          if (j > i && j < m && !removed[j] && iou_gt(bi, ai, box_at(j), p.thr)) bits |= 1u << q;
+        }
+      }
+      cmask[lane][wave] = (unsigned char)bits;
+    }
+    __syncthreads();
+    // (b) wave 0 resolves the chunk: pure mask arithmetic on a wave-uniform live set
+    if (wave == 0) {
+      const int i = c0 + lane;
+      uint64_t rm = 0;
+#pragma unroll
+      for (int w = 0; w < 16; ++w) rm |= (uint64_t)cmask[lane][w] << (4 * w);
+      const bool live = i < m && !removed[i];
+      uint64_t M = __ballot(live);
+      int nk = nk0, ck = 0;
+      while (M && nk < p.max_det) {
+        const int t = __ffsll((long long)M) - 1;
+        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rm, t);
+        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(rm >> 32), t);
+        if (lane == t) {
+          kept_sorted[nk] = i;
+          chunk_box[ck] = box_at(i);
+        }
+        M &= ~(((uint64_t)hi << 32) | lo);
+        M &= ~(1ull << t);
+        ++nk; ++ck;
+      }
+      if (lane == 0) s_nk = nk;
+    }
+    __syncthreads();
+    const int ck = s_nk - nk0;
+    if (s_nk >= p.max_det) break;
+    // (c) suppress every later box against the chunk's kept boxes (all of which precede it)
+    for (int j = c0 + 64 + threadIdx.x; j < m; j += NMS_THREADS) {
+      if (removed[j]) continue;
+      const f32x4 bj = box_at(j);
+      for (int q = 0; q < ck; ++q) {
+        const f32x4 bq = chunk_box[q];
+        const float aq = (bq[2] - bq[0]) * (bq[3] - bq[1]);
+        if (iou_gt(bq, aq, bj, p.thr)) {
+          removed[j] = 1;
           break;
         }
       }
-      if (lane == 0) s_next = found;
-    }
-    __syncthreads();
-    const int i = s_next;
-    __syncthreads();
-    if (i >= n || kept >= p.max_det) break;
-    if (threadIdx.x == 0) kept_slot[kept] = vb[i];
-    ++kept;
-    cur = i + 1;
-    const f32x4 bi = i < NMS_LDS_BOXES ? sbox[i] : load_box(i);
-    const float area_i = (bi[2] - bi[0]) * (bi[3] - bi[1]);
-    for (int j = i + 1 + threadIdx.x; j < n; j += blockDim.x) {
-      if (removed[j]) continue;
-      const f32x4 bj = j < NMS_LDS_BOXES ? sbox[j] : load_box(j);
-      const float xx1 = fmaxf(bi[0], bj[0]), yy1 = fmaxf(bi[1], bj[1]);
-      const float xx2 = fminf(bi[2], bj[2]), yy2 = fminf(bi[3], bj[3]);
-      const float ww = fmaxf(0.f, xx2 - xx1), hh = fmaxf(0.f, yy2 - yy1);
-      const float inter = ww * hh;
-      const float area_j = (bj[2] - bj[0]) * (bj[3] - bj[1]);
-      const float ovr = inter / ((area_i + area_j) - inter);
-      if ((double)ovr > p.thr) removed[j] = 1;
     }
     __syncthreads();
   }
-  for (int k = threadIdx.x; k < kept; k += blockDim.x) {
-    const int64_t o = (int64_t)b * p.cap + kept_slot[k];
+  __syncthreads();
+  const int kept = min(s_nk, p.max_det);
+  for (int k = threadIdx.x; k < kept; k += NMS_THREADS) {
+    const int slot = order[kept_sorted[k]];
+    const int64_t o = (int64_t)b * p.cap + slot;
     f32x4 v = *reinterpret_cast<const f32x4*>(p.cbox + o * 4);
     if (p.clip_w > 0.f) {
       v[0] = fminf(fmaxf(v[0], 0.f), p.clip_w);
@@ -387,8 +432,8 @@ extern "C" int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream) 
 
 extern "C" int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms) {
   (void)max_nms;
-  const int L = next_pow2(cap < SORT_CHUNK ? SORT_CHUNK : cap);
-  return (int64_t)n * L * (8 + 4);
+  if (cap <= NMS_SORT_LDS) return 16;
+  return (int64_t)n * next_pow2(cap) * (8 + 4);
 }
 
 extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
@@ -401,25 +446,17 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   if (d->max_nms < 1 || d->max_nms > NMS_MAX_FLAGS) return fail(YDBL_EINVAL, "nms: max_nms must be in [1, 32768]");
   if (!(d->iou_thres >= 0.0 && d->iou_thres <= 1.0)) return fail(YDBL_EINVAL, "nms: iou_thres must be in [0, 1]");
   hipStream_t s = as_stream(stream);
-  const int L = next_pow2(d->cap < SORT_CHUNK ? SORT_CHUNK : d->cap);
-  uint64_t* keys = reinterpret_cast<uint64_t*>(d->workspace);
-  int* vals = reinterpret_cast<int*>(keys + (int64_t)d->n * L);
-  nms_keys_kernel<<<dim3((unsigned)cdiv(L, 1024), d->n), 1024, 0, s>>>(d->cand_score, d->cand_idx, d->cand_count,
-                                                                       d->cap, L, keys, vals);
-  const int chunk = SORT_CHUNK;
-  bitonic_local_kernel<<<dim3(L / chunk, d->n), 1024, 0, s>>>(keys, vals, L, chunk, 0);
-  for (int k = 2 * chunk; k <= L; k <<= 1) {
-    for (int j = k >> 1; j >= chunk; j >>= 1)
-      bitonic_global_kernel<<<dim3((unsigned)cdiv(L / 2, 256), d->n), 256, 0, s>>>(keys, vals, L, k, j);
-    bitonic_local_kernel<<<dim3(L / chunk, d->n), 1024, 0, s>>>(keys, vals, L, chunk, k);
-  }
   NmsArgs a;
-  a.cbox = d->cand_box; a.cscore = d->cand_score; a.ccls = d->cand_cls; a.ccount = d->cand_count;
-  a.vals = vals; a.L = L; a.cap = d->cap;
+  a.cbox = d->cand_box; a.cscore = d->cand_score; a.ccls = d->cand_cls; a.cidx = d->cand_idx;
+  a.ccount = d->cand_count;
+  a.L = d->cap <= NMS_SORT_LDS ? 0 : next_pow2(d->cap);
+  a.gkeys = reinterpret_cast<uint64_t*>(d->workspace);
+  a.gvals = reinterpret_cast<int*>(a.gkeys + (int64_t)d->n * a.L);
+  a.cap = d->cap;
   a.thr = d->iou_thres; a.max_det = d->max_det; a.max_nms = d->max_nms;
   a.off_scale = d->agnostic ? 0.f : d->max_wh;
   a.clip_w = d->clip_w; a.clip_h = d->clip_h;
   a.out = d->out; a.out_count = d->out_count;
-  nms_greedy_kernel<<<d->n, 1024, 0, s>>>(a);
+  nms_kernel<<<d->n, NMS_THREADS, 0, s>>>(a);
   return check_launch("ydbl_nms");
 }

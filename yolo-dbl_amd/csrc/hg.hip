@@ -11,202 +11,301 @@
 // projection runs on E rows per image instead of N (exact in real arithmetic).
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace ydbl {
 
+// Token slices: image b's N tokens are split into NS slices so that B*NS workgroups fill the chip;
+// every reduction over N writes per-slice partials that the next stage combines in fixed order.
+static int hg_splits(int B, int N) {
+  int ns = (2048 + B - 1) / B;
+  const int max_ns = (N + 31) / 32;
+  if (ns > max_ns) ns = max_ns;
+  return ns < 1 ? 1 : ns;
+}
+constexpr int HG_LOGIT_TOK = 256;  // tokens per logits workgroup (one per thread)
+
 struct HgWs {
-  float* ctx;     // [B][2D]
+  float* ctxp;    // [B][NS][2D]   partial (sum, max) over a token slice
   float* proto;   // [B][E][D]
   float* logits;  // [B][N][E]
-  float* stats;   // [B][E][2]  (max, 1/sum)
-  float* he;      // [B][E][D]
+  float* lstat;   // [B][NL][E][2] partial (max, sum exp) per logits workgroup
+  float* stats;   // [B][E][2]     (max, 1/sum)
+  float* hep;     // [B][NS][E][D] partial A^T X
   float* he3;     // [B][E][D]
+  int ns, nl;
 };
 
 static HgWs carve(void* ws, int B, int N, int D, int E) {
   float* p = reinterpret_cast<float*>(ws);
   HgWs w;
-  w.ctx = p; p += (int64_t)B * 2 * D;
+  w.ns = hg_splits(B, N);
+  w.nl = (N + HG_LOGIT_TOK - 1) / HG_LOGIT_TOK;
+  w.ctxp = p; p += (int64_t)B * w.ns * 2 * D;
   w.proto = p; p += (int64_t)B * E * D;
   w.logits = p; p += (int64_t)B * N * E;
+  w.lstat = p; p += (int64_t)B * w.nl * E * 2;
   w.stats = p; p += (int64_t)B * E * 2;
-  w.he = p; p += (int64_t)B * E * D;
+  w.hep = p; p += (int64_t)B * w.ns * E * D;
   w.he3 = p;
   return w;
 }
 
+static int64_t hg_ws_floats(int B, int N, int D, int E) {
+  const int ns = hg_splits(B, N), nl = (N + HG_LOGIT_TOK - 1) / HG_LOGIT_TOK;
+  return (int64_t)B * ns * 2 * D + (int64_t)B * E * D + (int64_t)B * N * E + (int64_t)B * nl * E * 2 +
+         (int64_t)B * E * 2 + (int64_t)B * ns * E * D + (int64_t)B * E * D;
+}
+
+// partial context over one token slice: threads = (channel vector cv, token lane tl)
 template <typename T>
-__global__ __launch_bounds__(256) void hg_stats_kernel(DView<const T> x, float* __restrict__ ctx) {
-  __shared__ float ssum[4][64], smax[4][64];
-  const int b = blockIdx.x;
-  const int tx = threadIdx.x & 63, part = threadIdx.x >> 6;
-  const int d = blockIdx.y * 64 + tx;
+__global__ __launch_bounds__(256) void hg_stats_kernel(DView<const T> x, float* __restrict__ ctxp, int ns) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float ssum[256][V], smax[256][V];
+  const int b = blockIdx.y, k = blockIdx.x;
   const int N = x.h * x.w, D = x.c;
-  float s = 0.f, m = -INFINITY;
-  if (d < D) {
-    const T* base = x.p + (int64_t)b * N * x.cs + d;
-    for (int n = part; n < N; n += 4) {
-      const float v = float(base[(int64_t)n * x.cs]);
-      s += v;
-      m = fmaxf(m, v);
+  const int ncv = D / V;
+  const int lanes = 256 / ncv;  // token lanes (D <= 2048)
+  const int cv = threadIdx.x % ncv, tl = threadIdx.x / ncv;
+  const int n0 = (int)((int64_t)N * k / ns), n1 = (int)((int64_t)N * (k + 1) / ns);
+  float s[V], m[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) { s[q] = 0.f; m[q] = -INFINITY; }
+  if (tl < lanes) {
+    const T* base = x.p + (int64_t)b * N * x.cs + cv * V;
+    for (int n = n0 + tl; n < n1; n += lanes) {
+      float v[V];
+      load_f<V>(base + (int64_t)n * x.cs, v);
+#pragma unroll
+      for (int q = 0; q < V; ++q) { s[q] += v[q]; m[q] = fmaxf(m[q], v[q]); }
     }
   }
-  ssum[part][tx] = s;
-  smax[part][tx] = m;
+#pragma unroll
+  for (int q = 0; q < V; ++q) { ssum[threadIdx.x][q] = s[q]; smax[threadIdx.x][q] = m[q]; }
   __syncthreads();
-  if (part == 0 && d < D) {
-    const float st = (ssum[0][tx] + ssum[1][tx]) + (ssum[2][tx] + ssum[3][tx]);
-    const float mt = fmaxf(fmaxf(smax[0][tx], smax[1][tx]), fmaxf(smax[2][tx], smax[3][tx]));
-    ctx[(int64_t)b * 2 * D + d] = st / float(N);
-    ctx[(int64_t)b * 2 * D + D + d] = mt;
+  if (threadIdx.x < ncv) {
+    for (int t = 1; t < lanes; ++t) {
+#pragma unroll
+      for (int q = 0; q < V; ++q) {
+        s[q] += ssum[t * ncv + cv][q];
+        m[q] = fmaxf(m[q], smax[t * ncv + cv][q]);
+      }
+    }
+    float* o = ctxp + ((int64_t)b * ns + k) * 2 * D;
+#pragma unroll
+    for (int q = 0; q < V; ++q) { o[cv * V + q] = s[q]; o[D + cv * V + q] = m[q]; }
   }
 }
 
-// one wave per output row o = e*D + d of the context Linear; lanes split the 2D inputs
-__global__ __launch_bounds__(256) void hg_proto_kernel(const float* __restrict__ ctx, const float* __restrict__ w,
-                                                       const float* __restrict__ bias, const float* __restrict__ base,
-                                                       float* __restrict__ proto, int D, int E) {
+// proto[b][e][d] = base + ctx @ Wc^T + bc; ctx = [sum/N | max] combined from the slice partials.
+// one wave per output row o = e*D + d; lanes split the 2D inputs
+__global__ __launch_bounds__(256) void hg_proto_kernel(const float* __restrict__ ctxp, int ns, int N,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       const float* __restrict__ base, float* __restrict__ proto,
+                                                       int D, int E) {
+  extern __shared__ float sctx[];  // [2D]
   const int b = blockIdx.x;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int o = blockIdx.y * 4 + wave;
-  if (o >= E * D) return;
   const int K = 2 * D;
-  const float* c = ctx + (int64_t)b * K;
-  const float* wr = w + (int64_t)o * K;
-  float s = 0.f;
-  for (int k = lane; k < K; k += 64) s = fmaf(wr[k], c[k], s);
+  for (int i = threadIdx.x; i < K; i += blockDim.x) {
+    const float* c = ctxp + (int64_t)b * ns * K + i;
+    float v = c[0];
+    if (i < D) {
+      for (int k = 1; k < ns; ++k) v += c[(int64_t)k * K];
+      v /= float(N);
+    } else {
+      for (int k = 1; k < ns; ++k) v = fmaxf(v, c[(int64_t)k * K]);
+    }
+    sctx[i] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int o = blockIdx.y * 4 + wave; o < E * D; o += gridDim.y * 4) {
+    const float* wr = w + (int64_t)o * K;
+    float s = 0.f;
+    for (int k = lane; k < K; k += 64) s = fmaf(wr[k], sctx[k], s);
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  if (lane == 0) proto[(int64_t)b * E * D + o] = base[o] + (s + bias[o]);
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) proto[(int64_t)b * E * D + o] = base[o] + (s + bias[o]);
+  }
 }
 
+// logits[n][e] = mean_h (xp_h[n] . proto_h[e]) / sqrt(head_dim), plus per-workgroup softmax partials
 template <typename T, int E>
-__global__ __launch_bounds__(256) void hg_logits_kernel(DView<const T> xp, const float* __restrict__ proto,
-                                                        float* __restrict__ logits, int H, float inv_scale) {
+__global__ __launch_bounds__(HG_LOGIT_TOK) void hg_logits_kernel(DView<const T> xp, const float* __restrict__ proto,
+                                                                 float* __restrict__ logits, float* __restrict__ lstat,
+                                                                 int H, float inv_scale) {
   extern __shared__ float sp[];  // [E][D]
+  __shared__ float red[E][HG_LOGIT_TOK / 64];
+  __shared__ float smx[E];
   const int b = blockIdx.y;
   const int D = xp.c, N = xp.h * xp.w;
   for (int i = threadIdx.x; i < E * D; i += blockDim.x) sp[i] = proto[(int64_t)b * E * D + i];
   __syncthreads();
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
   constexpr int V = Vec<T>::N;
   const int hd = D / H;
-  const T* row = xp.p + ((int64_t)b * N + n) * xp.cs;
-  float tot[E], head[E];
+  float tot[E];
 #pragma unroll
-  for (int e = 0; e < E; ++e) tot[e] = head[e] = 0.f;
-  for (int d0 = 0; d0 < D; d0 += V) {
-    float v[V];
-    load_f<V>(row + d0, v);
+  for (int e = 0; e < E; ++e) tot[e] = -INFINITY;
+  if (n < N) {
+    const T* row = xp.p + ((int64_t)b * N + n) * xp.cs;
+    float head[E];
 #pragma unroll
-    for (int q = 0; q < V; ++q) {
-      const int d = d0 + q;
+    for (int e = 0; e < E; ++e) tot[e] = head[e] = 0.f;
+    for (int d0 = 0; d0 < D; d0 += V) {
+      float v[V];
+      load_f<V>(row + d0, v);
 #pragma unroll
-      for (int e = 0; e < E; ++e) head[e] = fmaf(v[q], sp[e * D + d], head[e]);
-      if ((d + 1) % hd == 0) {
+      for (int q = 0; q < V; ++q) {
+        const int d = d0 + q;
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-          tot[e] += head[e] * inv_scale;
-          head[e] = 0.f;
+        for (int e = 0; e < E; ++e) head[e] = fmaf(v[q], sp[e * D + d], head[e]);
+        if ((d + 1) % hd == 0) {
+#pragma unroll
+          for (int e = 0; e < E; ++e) {
+            tot[e] += head[e] * inv_scale;
+            head[e] = 0.f;
+          }
         }
       }
     }
-  }
-  float* lo = logits + ((int64_t)b * N + n) * E;
+    float* lo = logits + ((int64_t)b * N + n) * E;
 #pragma unroll
-  for (int e = 0; e < E; ++e) lo[e] = tot[e] / float(H);
-}
-
-template <int E>
-__global__ __launch_bounds__(256) void hg_softmax_kernel(const float* __restrict__ logits, float* __restrict__ stats,
-                                                         int N) {
-  __shared__ float red[E][256];
-  const int b = blockIdx.x;
-  const float* l = logits + (int64_t)b * N * E;
-  float m[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) m[e] = -INFINITY;
-  for (int n = threadIdx.x; n < N; n += 256)
-#pragma unroll
-    for (int e = 0; e < E; ++e) m[e] = fmaxf(m[e], l[(int64_t)n * E + e]);
-#pragma unroll
-  for (int e = 0; e < E; ++e) red[e][threadIdx.x] = m[e];
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s)
-#pragma unroll
-      for (int e = 0; e < E; ++e) red[e][threadIdx.x] = fmaxf(red[e][threadIdx.x], red[e][threadIdx.x + s]);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int e = 0; e < E; ++e) m[e] = red[e][0];
-  __syncthreads();
-  float sum[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) sum[e] = 0.f;
-  for (int n = threadIdx.x; n < N; n += 256)
-#pragma unroll
-    for (int e = 0; e < E; ++e) sum[e] += expf(l[(int64_t)n * E + e] - m[e]);
-#pragma unroll
-  for (int e = 0; e < E; ++e) red[e][threadIdx.x] = sum[e];
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s)
-#pragma unroll
-      for (int e = 0; e < E; ++e) red[e][threadIdx.x] += red[e][threadIdx.x + s];
-    __syncthreads();
-  }
-  if (threadIdx.x < E) {
-    stats[((int64_t)b * E + threadIdx.x) * 2 + 0] = m[threadIdx.x];
-    stats[((int64_t)b * E + threadIdx.x) * 2 + 1] = 1.0f / red[threadIdx.x][0];
-  }
-}
-
-// He[b][e][d] = sum_n A[n][e] * X[n][d]
-template <typename T, int E>
-__global__ __launch_bounds__(256) void hg_gather_kernel(DView<const T> x, const float* __restrict__ logits,
-                                                        const float* __restrict__ stats, float* __restrict__ he) {
-  __shared__ float red[4][E][64];
-  const int b = blockIdx.x;
-  const int tx = threadIdx.x & 63, part = threadIdx.x >> 6;
-  const int d = blockIdx.y * 64 + tx;
-  const int N = x.h * x.w, D = x.c;
-  float mx[E], inv[E], acc[E];
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    mx[e] = stats[((int64_t)b * E + e) * 2];
-    inv[e] = stats[((int64_t)b * E + e) * 2 + 1];
-    acc[e] = 0.f;
-  }
-  const float* l = logits + (int64_t)b * N * E;
-  const T* xb = x.p + (int64_t)b * N * x.cs;
-  if (d < D) {
-    for (int n = part; n < N; n += 4) {
-      const float xv = float(xb[(int64_t)n * x.cs + d]);
-#pragma unroll
-      for (int e = 0; e < E; ++e) acc[e] = fmaf(expf(l[(int64_t)n * E + e] - mx[e]) * inv[e], xv, acc[e]);
+    for (int e = 0; e < E; ++e) {
+      tot[e] = tot[e] / float(H);
+      lo[e] = tot[e];
     }
   }
+  // workgroup partial softmax stats: max, then sum exp(l - max)
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int e = 0; e < E; ++e) red[part][e][tx] = acc[e];
+  for (int e = 0; e < E; ++e) {
+    float m = tot[e];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off, 64));
+    if (lane == 0) red[e][wave] = m;
+  }
   __syncthreads();
-  if (part == 0 && d < D) {
+  if (threadIdx.x < E) {
+    float m = red[threadIdx.x][0];
+    for (int w2 = 1; w2 < HG_LOGIT_TOK / 64; ++w2) m = fmaxf(m, red[threadIdx.x][w2]);
+    smx[threadIdx.x] = m;
+  }
+  __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-      he[((int64_t)b * E + e) * D + d] = (red[0][e][tx] + red[1][e][tx]) + (red[2][e][tx] + red[3][e][tx]);
+  for (int e = 0; e < E; ++e) {
+    float v = n < N ? expf(tot[e] - smx[e]) : 0.f;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) red[e][wave] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < E) {
+    float sum = red[threadIdx.x][0];
+    for (int w2 = 1; w2 < HG_LOGIT_TOK / 64; ++w2) sum += red[threadIdx.x][w2];
+    float* o = lstat + (((int64_t)b * gridDim.x + blockIdx.x) * E + threadIdx.x) * 2;
+    o[0] = smx[threadIdx.x];
+    o[1] = sum;
+  }
+}
+
+// softmax over N from the logits partials: (max, 1/sum) per (image, hyperedge)
+template <int E>
+__device__ __forceinline__ void combine_stats(const float* __restrict__ lstat, int b, int nl, float* mx, float* inv) {
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    float m = -INFINITY;
+    for (int k = 0; k < nl; ++k) m = fmaxf(m, lstat[(((int64_t)b * nl + k) * E + e) * 2]);
+    float sum = 0.f;
+    for (int k = 0; k < nl; ++k) {
+      const float* st = lstat + (((int64_t)b * nl + k) * E + e) * 2;
+      sum += st[1] * expf(st[0] - m);
+    }
+    mx[e] = m;
+    inv[e] = 1.0f / sum;
+  }
+}
+
+// partial He[b][k][e][d] = sum_{n in slice k} A[n][e] * X[n][d]
+template <typename T, int E>
+__global__ __launch_bounds__(256) void hg_gather_kernel(DView<const T> x, const float* __restrict__ logits,
+                                                        const float* __restrict__ lstat, int nl,
+                                                        float* __restrict__ hep, int ns) {
+  constexpr int V = Vec<T>::N;
+  __shared__ float s_mx[E], s_inv[E];
+  __shared__ float red[256][V];
+  const int b = blockIdx.y, k = blockIdx.x;
+  const int N = x.h * x.w, D = x.c;
+  if (threadIdx.x == 0) combine_stats<E>(lstat, b, nl, s_mx, s_inv);
+  __syncthreads();
+  const int ncv = D / V;
+  const int lanes = 256 / ncv;
+  const int cv = threadIdx.x % ncv, tl = threadIdx.x / ncv;
+  const int n0 = (int)((int64_t)N * k / ns), n1 = (int)((int64_t)N * (k + 1) / ns);
+  float acc[E][V];
+#pragma unroll
+  for (int e = 0; e < E; ++e)
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[e][q] = 0.f;
+  if (tl < lanes) {
+    const T* xb = x.p + (int64_t)b * N * x.cs + cv * V;
+    const float* l = logits + (int64_t)b * N * E;
+    for (int n = n0 + tl; n < n1; n += lanes) {
+      float xv[V];
+      load_f<V>(xb + (int64_t)n * x.cs, xv);
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        const float a = expf(l[(int64_t)n * E + e] - s_mx[e]) * s_inv[e];
+#pragma unroll
+        for (int q = 0; q < V; ++q) acc[e][q] = fmaf(a, xv[q], acc[e][q]);
+      }
+    }
+  }
+  float* o = hep + ((int64_t)b * ns + k) * E * D;
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+#pragma unroll
+    for (int q = 0; q < V; ++q) red[threadIdx.x][q] = acc[e][q];
+    __syncthreads();
+    if (threadIdx.x < ncv) {
+      float v[V];
+#pragma unroll
+      for (int q = 0; q < V; ++q) v[q] = red[cv][q];
+      for (int t = 1; t < lanes; ++t)
+#pragma unroll
+        for (int q = 0; q < V; ++q) v[q] += red[t * ncv + cv][q];
+#pragma unroll
+      for (int q = 0; q < V; ++q) o[e * D + cv * V + q] = v[q];
+    }
+    __syncthreads();
   }
 }
 
 // He2 = GELU(He @ We^T + be); He3 = He2 @ Wn^T   (per image, E rows)
 template <int E>
-__global__ __launch_bounds__(256) void hg_edge_kernel(const float* __restrict__ he, const float* __restrict__ we,
+__global__ __launch_bounds__(256) void hg_edge_kernel(const float* __restrict__ hep, int ns,
+                                                      const float* __restrict__ lstat, int nl,
+                                                      float* __restrict__ stats, const float* __restrict__ we,
                                                       const float* __restrict__ be, const float* __restrict__ wn,
                                                       float* __restrict__ he3, int D) {
   extern __shared__ float sm[];  // he [E][D], he2 [E][D]
   float* sh = sm;
   float* sh2 = sm + E * D;
   const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < E * D; i += blockDim.x) sh[i] = he[(int64_t)b * E * D + i];
+  for (int i = threadIdx.x; i < E * D; i += blockDim.x) {
+    const float* p = hep + (int64_t)b * ns * E * D + i;
+    float v = p[0];
+    for (int k = 1; k < ns; ++k) v += p[(int64_t)k * E * D];
+    sh[i] = v;
+  }
+  if (threadIdx.x == 0) {
+    float mx[E], inv[E];
+    combine_stats<E>(lstat, b, nl, mx, inv);
+    for (int e = 0; e < E; ++e) {
+      stats[((int64_t)b * E + e) * 2] = mx[e];
+      stats[((int64_t)b * E + e) * 2 + 1] = inv[e];
+    }
+  }
   __syncthreads();
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     const float* wr = we + (int64_t)d * D;
@@ -275,9 +374,10 @@ template <typename T, int E>
 static int hg_context_t(const ydbl_hg_desc* d, hipStream_t s) {
   const int B = d->x.n, N = d->x.h * d->x.w, D = d->x.c;
   HgWs w = carve(d->workspace, B, N, D, E);
-  hg_stats_kernel<T><<<dim3(B, (unsigned)cdiv(D, 64)), 256, 0, s>>>(cv<T>(d->x), w.ctx);
-  hg_proto_kernel<<<dim3(B, (unsigned)cdiv(E * D, 4)), 256, 0, s>>>(w.ctx, d->ctx_w, d->ctx_b, d->proto_base, w.proto,
-                                                                     D, E);
+  hg_stats_kernel<T><<<dim3(w.ns, B), 256, 0, s>>>(cv<T>(d->x), w.ctxp, w.ns);
+  const int rows_blocks = (int)std::min<int64_t>(cdiv(E * D, 4), std::max<int64_t>(1, cdiv(1024, B)));
+  hg_proto_kernel<<<dim3(B, rows_blocks), 256, 2 * D * sizeof(float), s>>>(w.ctxp, w.ns, N, d->ctx_w, d->ctx_b,
+                                                                           d->proto_base, w.proto, D, E);
   return check_launch("ydbl_hg_context");
 }
 
@@ -286,11 +386,11 @@ static int hg_propagate_t(const ydbl_hg_desc* d, hipStream_t s) {
   const int B = d->x.n, N = d->x.h * d->x.w, D = d->x.c, H = d->num_heads;
   HgWs w = carve(d->workspace, B, N, D, E);
   const float inv_scale = 1.0f / sqrtf(float(D / H));
-  hg_logits_kernel<T, E><<<dim3((unsigned)cdiv(N, 256), B), 256, E * D * sizeof(float), s>>>(cv<T>(d->xp), w.proto,
-                                                                                               w.logits, H, inv_scale);
-  hg_softmax_kernel<E><<<B, 256, 0, s>>>(w.logits, w.stats, N);
-  hg_gather_kernel<T, E><<<dim3(B, (unsigned)cdiv(D, 64)), 256, 0, s>>>(cv<T>(d->x), w.logits, w.stats, w.he);
-  hg_edge_kernel<E><<<B, 256, 2 * E * D * sizeof(float), s>>>(w.he, d->edge_w, d->edge_b, d->node_w, w.he3, D);
+  hg_logits_kernel<T, E><<<dim3(w.nl, B), HG_LOGIT_TOK, E * D * sizeof(float), s>>>(cv<T>(d->xp), w.proto, w.logits,
+                                                                                     w.lstat, H, inv_scale);
+  hg_gather_kernel<T, E><<<dim3(w.ns, B), 256, 0, s>>>(cv<T>(d->x), w.logits, w.lstat, w.nl, w.hep, w.ns);
+  hg_edge_kernel<E><<<B, 256, 2 * E * D * sizeof(float), s>>>(w.hep, w.ns, w.lstat, w.nl, w.stats, d->edge_w,
+                                                               d->edge_b, d->node_w, w.he3, D);
   const int V = Vec<T>::N;
   hg_out_kernel<T, E><<<(unsigned)cdiv((int64_t)B * N * (D / V), 256), 256, 0, s>>>(
       cv<T>(d->x), w.logits, w.stats, w.he3, d->node_b, dview<T>(d->y));
@@ -333,7 +433,7 @@ static int by_edges(int e, F&& f) {
 using namespace ydbl;
 
 extern "C" int64_t ydbl_hg_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges) {
-  return 4 * ((int64_t)n * 2 * dim + 3LL * n * edges * dim + (int64_t)n * tokens * edges + 2LL * n * edges);
+  return 4 * hg_ws_floats(n, tokens, dim, edges);
 }
 
 extern "C" int ydbl_hg_context(const ydbl_hg_desc* d, void* stream) {

@@ -54,6 +54,132 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DView<const T> x, DView<T> 
   store_f<V>(y.at(b, oy, ox) + c0, acc);
 }
 
+// LDS-tiled variant for the fixed geometries of the DBL graphs.  A workgroup owns a TH x TW output
+// tile x CV channel vectors (16 B each); the input tile it needs, halo included, is staged in LDS
+// once with coalesced 16-byte loads (one global read per input element instead of one per tap), then
+// every thread computes its outputs from LDS.  Accumulation order per output is the reference's tap
+// order (ky, kx) with padded taps skipped, identical to dwconv_kernel.
+template <typename T, int K, int S, int DIL, int CV, int TH, int TW>
+__global__ __launch_bounds__(256) void dwconv_lds_kernel(DView<const T> x, DView<T> y, DView<const T> r,
+                                                         const float* __restrict__ w, const float* __restrict__ bias,
+                                                         int PAD, int act, int tiles_x, int tiles_y) {
+  constexpr int V = Vec<T>::N;
+  constexpr int IH = (TH - 1) * S + (K - 1) * DIL + 1;
+  constexpr int IW = (TW - 1) * S + (K - 1) * DIL + 1;
+  constexpr int LANES = 256 / CV;             // pixel lanes
+  constexpr int NPX = (TH * TW) / LANES;      // outputs per thread, computed jointly
+  static_assert(NPX * LANES == TH * TW, "tile must split evenly over the pixel lanes");
+  using vec = typename Vec<T>::type;
+  __shared__ vec tile[IH * IW * CV];
+  __shared__ f32x4 wts[K * K * CV * V / 4];   // fp32 taps of this workgroup's channel slice
+  const int cgroups = y.c / (CV * V);
+  int bid = blockIdx.x;
+  const int cgi = bid % cgroups; bid /= cgroups;
+  const int tx = bid % tiles_x; bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int c0 = cgi * CV * V;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - PAD, ix0 = ox0 * S - PAD;
+  {  // stage the halo tile: all loads of a thread in flight before the first LDS store
+    constexpr int TOT = IH * IW * CV, IT = (TOT + 255) / 256;
+    vec tmp[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int cv = i % CV, px = i / CV;
+      const int iy = iy0 + px / IW, ix = ix0 + px % IW;
+      tmp[it] = (i < TOT && iy >= 0 && iy < x.h && ix >= 0 && ix < x.w) ? vload(x.at(b, iy, ix) + c0 + cv * V)
+                                                                       : vzero<T>();
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (i < TOT) tile[i] = tmp[it];
+    }
+  }
+  for (int i = threadIdx.x; i < K * K * CV * V / 4; i += 256) {
+    const int tap = i / (CV * V / 4), q = i % (CV * V / 4);
+    wts[i] = *reinterpret_cast<const f32x4*>(w + tap * y.c + c0 + 4 * q);
+  }
+  __syncthreads();
+  const int cv = threadIdx.x % CV, pl = threadIdx.x / CV;
+  const int cc = c0 + cv * V;
+  int py[NPX], px[NPX];
+  bool ok[NPX];
+#pragma unroll
+  for (int u = 0; u < NPX; ++u) {
+    const int p = pl + u * LANES;
+    py[u] = p / TW; px[u] = p % TW;
+    ok[u] = oy0 + py[u] < y.h && ox0 + px[u] < y.w;
+  }
+  float acc[NPX][V];
+#pragma unroll
+  for (int u = 0; u < NPX; ++u)
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[u][q] = 0.f;
+#pragma unroll 1
+  for (int ky = 0; ky < K; ++ky) {
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) {
+      float wv[V];
+#pragma unroll
+      for (int h = 0; h < V / 4; ++h) {
+        const f32x4 t4 = wts[((ky * K + kx) * CV + cv) * (V / 4) + h];
+        wv[4 * h] = t4[0]; wv[4 * h + 1] = t4[1]; wv[4 * h + 2] = t4[2]; wv[4 * h + 3] = t4[3];
+      }
+#pragma unroll
+      for (int u = 0; u < NPX; ++u) {
+        const int iy = (oy0 + py[u]) * S - PAD + ky * DIL;
+        const int ix = (ox0 + px[u]) * S - PAD + kx * DIL;
+        if (iy < 0 || iy >= x.h || ix < 0 || ix >= x.w) continue;  // the reference has no padded-tap terms
+        const vec xv = tile[((py[u] * S + ky * DIL) * IW + px[u] * S + kx * DIL) * CV + cv];
+#pragma unroll
+        for (int q = 0; q < V; ++q) acc[u][q] = fmaf(float(xv[q]), wv[q], acc[u][q]);
+      }
+    }
+  }
+  float bv[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) bv[q] = 0.f;
+  if (bias) load_f<V>(bias + cc, bv);
+#pragma unroll
+  for (int u = 0; u < NPX; ++u) {
+    if (!ok[u]) continue;
+    const int oy = oy0 + py[u], ox = ox0 + px[u];
+    float o[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) o[q] = apply_act(bias ? acc[u][q] + bv[q] : acc[u][q], act);
+    if (r.p) {
+      float rv[V];
+      load_f<V>(r.at(b, oy, ox) + cc, rv);
+#pragma unroll
+      for (int q = 0; q < V; ++q) o[q] = rv[q] + o[q];
+    }
+    store_f<V>(y.at(b, oy, ox) + cc, o);
+  }
+}
+
+template <typename T>
+static bool launch_dw_lds(const ydbl_dwconv_desc* d, DView<const T> x, DView<T> y, DView<const T> r, hipStream_t s) {
+  constexpr int V = Vec<T>::N;
+  const int k = d->kw, st = d->stride, dl = d->dil;
+  auto go = [&](auto kern, int cv, int th, int tw) {
+    if (d->y.c % (cv * V)) return false;
+    const int tiles_x = (int)cdiv(d->y.w, tw), tiles_y = (int)cdiv(d->y.h, th);
+    const int64_t blocks = (int64_t)d->y.n * tiles_y * tiles_x * (d->y.c / (cv * V));
+    kern<<<(unsigned)blocks, 256, 0, s>>>(x, y, r, d->w, d->bias, d->pad, d->act, tiles_x, tiles_y);
+    return true;
+  };
+  // f16: 8 vectors = 64 channels per workgroup; f32: 8 vectors = 32 channels
+  if (k == 3 && st == 1 && dl == 1) return go(dwconv_lds_kernel<T, 3, 1, 1, 8, 8, 8>, 8, 8, 8);
+  if (k == 3 && st == 2 && dl == 1) return go(dwconv_lds_kernel<T, 3, 2, 1, 8, 8, 8>, 8, 8, 8);
+  if (k == 5 && st == 1 && dl == 1) return go(dwconv_lds_kernel<T, 5, 1, 1, 8, 8, 8>, 8, 8, 8);
+  if (k == 7 && st == 1 && dl == 1) return go(dwconv_lds_kernel<T, 7, 1, 1, 8, 8, 8>, 8, 8, 8);
+  if (k == 7 && st == 1 && dl == 3) return go(dwconv_lds_kernel<T, 7, 1, 3, 2, 8, 16>, 2, 8, 16);
+  return false;
+}
+
 // ------------------------------------------------------------------ input NCHW fp32 -> NHWC
 template <typename T>
 __global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x, int n, int c, int h, int w,
@@ -276,6 +402,14 @@ extern "C" int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream) {
   hipStream_t s = as_stream(stream);
   const int V = d->x.dtype == YDBL_F16 ? 8 : 4;
   const int64_t total = (int64_t)d->y.n * d->y.h * d->y.w * (d->y.c / V);
+  if (d->kh == d->kw) {
+    const bool done = d->x.dtype == YDBL_F16
+                          ? launch_dw_lds<_Float16>(d, cview<_Float16>(&d->x), dview<_Float16>(d->y),
+                                                   cview<_Float16>(res ? &d->r : nullptr), s)
+                          : launch_dw_lds<float>(d, cview<float>(&d->x), dview<float>(d->y),
+                                                cview<float>(res ? &d->r : nullptr), s);
+    if (done) return check_launch("ydbl_dwconv2d_nhwc");
+  }
   if (d->x.dtype == YDBL_F16)
     dwconv_kernel<_Float16><<<nblk(total), 256, 0, s>>>(cview<_Float16>(&d->x), dview<_Float16>(d->y),
                                                         cview<_Float16>(res ? &d->r : nullptr), d->w, d->bias,

@@ -75,6 +75,8 @@ SIGNATURES = {
     "ydbl_conv2d_nhwc": ([C.POINTER(ConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
+    "ydbl_conv_stem": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _P, _P, C.c_int32, C.c_int32,
+                        C.c_int32, _VP, _P], C.c_int),
     "ydbl_gate_add": ([_VP, _VP, C.c_float, _VP, _P], C.c_int),
     "ydbl_pool_up_concat": ([_VP, _VP, _VP, _VP, _P], C.c_int),
     "ydbl_dysample": ([_VP, _VP, C.c_int32, _VP, _P], C.c_int),

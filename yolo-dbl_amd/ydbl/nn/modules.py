@@ -121,6 +121,29 @@ def emit_conv2d(plan: Plan, conv: nn.Conv2d, x: TV, out: TV | None, weight=None,
     return y
 
 
+def stem_ok(m, ch: int) -> bool:
+    """The first layer can run as ydbl_conv_stem (3x3 Conv on the raw NCHW image)."""
+    if type(m) is not Conv:
+        return False
+    c = m.conv
+    return (c.groups == 1 and c.in_channels == ch and 1 <= ch <= 3 and c.kernel_size == (3, 3)
+            and c.padding == (1, 1) and c.dilation == (1, 1) and c.stride[0] == c.stride[1] in (1, 2)
+            and c.out_channels % 4 == 0 and c.out_channels <= 64 and isinstance(m.act, (nn.SiLU, nn.Identity)))
+
+
+def emit_stem(m: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: int, w: int) -> TV:
+    """preprocess (U/engine/predictor.py:116-134) + first Conv (conv.py:39-63, BN folded) in one kernel."""
+    wf, bf = m.folded()
+    s = m.conv.stride[0]
+    ho, wo = conv_out_hw(h, w, 3, s, 1, 1)
+    y = plan.alloc(n, ho, wo, m.conv.out_channels)
+    wd = plan.const(wf.float().contiguous())
+    bd = plan.const((bf if bf is not None else torch.zeros(m.conv.out_channels)).float())
+    plan.launch("ydbl_conv_stem", x_nchw.data_ptr(), n, ch, h, w, 1.0, wd.data_ptr(), bd.data_ptr(), 3, s,
+                _act_code(m.act), y.struct(), what="Stem.conv3x3", keep=[wd, bd])
+    return y
+
+
 def emit_seq(plan: Plan, mods, x, out=None):
     mods = list(mods)
     for i, m in enumerate(mods):

@@ -221,9 +221,15 @@ class DetectionModel(nn.Module):
                     off += c
         y: list[TV | None] = []
         x = inp
-        plan.launch("ydbl_input_nchw_to_nhwc", x_nchw.data_ptr(), batch, self.yaml["ch"], h, w, 1.0, inp.struct(),
-                    what="input")
+        stem = layers[0] if M.stem_ok(layers[0], self.yaml["ch"]) and 0 not in out_hint else None
+        if stem is None:
+            plan.launch("ydbl_input_nchw_to_nhwc", x_nchw.data_ptr(), batch, self.yaml["ch"], h, w, 1.0, inp.struct(),
+                        what="input")
         for m in layers:
+            if m is stem:  # preprocess + first Conv fused, straight from the NCHW batch
+                x = M.emit_stem(m, plan, x_nchw, batch, self.yaml["ch"], h, w)
+                y.append(x)
+                continue
             if m.f != -1:
                 x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
             out = cat_buf.get(m.i, out_hint.get(m.i))

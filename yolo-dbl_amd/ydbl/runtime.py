@@ -121,6 +121,9 @@ class Plan:
         stream = torch.cuda.current_stream(self.device)
         s = C.c_void_p(stream.cuda_stream)
         evs = []
+        # park the stream so the host enqueues every launch before the first one runs: the event
+        # pairs then time the kernels, not the host's launch latency
+        torch.cuda._sleep(int(1e8))
         for st in self.steps:
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
