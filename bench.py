@@ -166,14 +166,12 @@ def main():
     sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev)
     # synthetic images, different per rank, resident in the session's input buffer (HBM)
     sess.load(blob_images(B, S, seed=1234 + rank).to(dev))
-    gathered = [torch.empty_like(sess.det) for _ in range(world)] if world > 1 else None
-    counts = [torch.empty_like(sess.count) for _ in range(world)] if world > 1 else None
+    from ydbl.parallel import gather_detections
 
     def step():
-        det, cnt = sess()
-        if world > 1:
-            dist.all_gather(gathered, det)
-            dist.all_gather(counts, cnt)
+        det, cnt = sess()  # this rank's B images: forward + decode + NMS (one hipGraph replay)
+        if world > 1:  # the path's only exchange: one all-gather of the fixed-shape box buffers
+            gather_detections(det, cnt, B * world)
 
     for _ in range(args.warmup):
         step()

@@ -93,7 +93,7 @@ int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int
                             const ydbl_view* y, void* stream);
 
 /* Stem: y = act(conv_kxk(x * scale) + bias) straight from an NCHW fp32 batch x [n][cin][h][w]
- * (cin 1..3), w fp32 [cout][cin][k][k] (torch layout, BN folded), bias fp32 [cout]; y NHWC view with
+ * (cin = 3), w fp32 [cout][cin][k][k] (torch layout, BN folded), bias fp32 [cout]; y NHWC view with
  * y.c = cout (multiple of 4, <= 64); k = 3, pad = 1, stride 1 or 2.  In f16 mode the scaled input is rounded
  * to f16 before the conv (the reference's .half() input); arithmetic is fp32. */
 int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, float scale, const float* wt,

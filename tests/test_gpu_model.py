@@ -141,3 +141,50 @@ def test_predict_api(golden_dir):
     # uint8-range inputs are divided by 255 (LoadTensor)
     r255 = p.predict(x * 255.0, conf=0.05, half=True)
     assert torch.equal(r255[0].boxes.data, res[0].boxes.data)
+
+
+def _cpu_map50(o, x, labels):
+    """mAP@0.5 of the CPU oracle path under the same val protocol (multi-label NMS, conf .001)."""
+    from oracle.ops import clip_boxes, non_max_suppression
+    from ydbl.utils.metrics import IOUV, DetMetrics, box_iou, match_predictions
+
+    with torch.no_grad():
+        y, _ = o(x)
+    preds = non_max_suppression(y, 0.001, 0.7, multi_label=True)
+    st = {"tp": [], "conf": [], "pred_cls": [], "target_cls": []}
+    for i, p in enumerate(preds):
+        clip_boxes(p[:, :4], x.shape[2:])
+        cls, box = labels[i][:, 0], labels[i][:, 1:]
+        tp = match_predictions(p[:, 5], cls, box_iou(box, p[:, :4]), IOUV) if len(cls) and len(p) else \
+            torch.zeros(len(p), 10, dtype=torch.bool)
+        st["tp"].append(tp); st["conf"].append(p[:, 4]); st["pred_cls"].append(p[:, 5]); st["target_cls"].append(cls)
+    m = DetMetrics()
+    m.process(*(torch.cat(st[k]).numpy() for k in ("tp", "conf", "pred_cls", "target_cls")))
+    return m.box.map50
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_map50_gpu_vs_cpu_pseudo_gt(golden_dir, half):
+    """SURVEY §8d mAP protocol: pseudo ground truth = CPU oracle detections at conf 0.25; GPU and CPU
+    paths scored with the same val pipeline; acceptance |mAP50_gpu - mAP50_cpu| <= 0.1."""
+    from oracle.ops import clip_boxes, non_max_suppression
+    from ydbl.utils.synthetic import blob_images
+
+    p, o = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    x = blob_images(6, 256, seed=321)
+    with torch.no_grad():
+        y, _ = o(x)
+    gt = non_max_suppression(y, 0.25, 0.7)
+    labels = []
+    for g in gt:
+        clip_boxes(g[:, :4], (256, 256))
+        labels.append(torch.cat([g[:, 5:6], g[:, :4]], 1))
+    assert sum(len(lb) for lb in labels) > 0, "pseudo ground truth is empty"
+    batch = {"img": x, "cls": torch.cat([lb[:, 0] for lb in labels]),
+             "bboxes": torch.cat([lb[:, 1:] for lb in labels]),
+             "batch_idx": torch.cat([torch.full((len(lb),), i) for i, lb in enumerate(labels)])}
+    m_gpu = p.val(data=[batch], half=half).box.map50
+    m_cpu = _cpu_map50(o, x, labels)
+    print(f"mAP50 pseudo-GT: gpu({'fp16' if half else 'fp32'}) {m_gpu:.4f}  cpu {m_cpu:.4f}")
+    assert abs(m_gpu - m_cpu) <= 0.1
+    assert m_cpu > 0.5

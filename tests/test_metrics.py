@@ -1,0 +1,52 @@
+"""mAP machinery (host numpy restatement of U/utils/metrics.py / U/engine/validator.py) on
+hand-checkable cases."""
+
+import numpy as np
+import torch
+
+
+def test_box_iou_known_values():
+    from ydbl.utils.metrics import box_iou
+
+    a = torch.tensor([[0.0, 0.0, 10.0, 10.0]])
+    b = torch.tensor([[0.0, 0.0, 10.0, 10.0], [5.0, 0.0, 15.0, 10.0], [20.0, 20.0, 30.0, 30.0]])
+    iou = box_iou(a, b)[0]
+    assert abs(iou[0].item() - 1.0) < 1e-6
+    assert abs(iou[1].item() - 50.0 / 150.0) < 1e-6
+    assert iou[2].item() == 0.0
+
+
+def test_compute_ap_perfect_and_half():
+    from ydbl.utils.metrics import compute_ap
+
+    # the reference's sentinels (recall 1 -> precision 0) make a perfect curve 0.995 on the 101-point grid
+    ap, _, _ = compute_ap(np.array([0.5, 1.0]), np.array([1.0, 1.0]))
+    assert abs(ap - 0.995) < 1e-9
+    # precision 1 up to recall 0.5, then the interpolation runs linearly to (1, 0): 0.5 + 0.25
+    ap, _, _ = compute_ap(np.array([0.5]), np.array([1.0]))
+    assert abs(ap - 0.75) < 1e-9
+
+
+def test_match_predictions_greedy_unique():
+    from ydbl.utils.metrics import IOUV, box_iou, match_predictions
+
+    gt = torch.tensor([[0.0, 0.0, 10.0, 10.0]])
+    gcls = torch.tensor([1.0])
+    pred = torch.tensor([[0.0, 0.0, 10.0, 10.0], [0.0, 0.0, 10.0, 9.0], [0.0, 0.0, 10.0, 10.0]])
+    pcls = torch.tensor([1.0, 1.0, 0.0])
+    tp = match_predictions(pcls, gcls, box_iou(gt, pred), IOUV)
+    assert tp[0].all()  # exact box, matched at every threshold
+    assert not tp[1].any()  # the label is already taken by the better match
+    assert not tp[2].any()  # wrong class
+
+
+def test_ap_per_class_two_classes():
+    from ydbl.utils.metrics import ap_per_class
+
+    tp = np.array([[True] * 10, [False] * 10, [True] * 10])
+    conf = np.array([0.9, 0.8, 0.7])
+    pred_cls = np.array([0, 0, 1])
+    target_cls = np.array([0, 1])
+    *_, ap, classes = ap_per_class(tp, conf, pred_cls, target_cls)
+    assert list(classes) == [0, 1]
+    assert abs(ap[0, 0] - 0.995) < 1e-6 and abs(ap[1, 0] - 0.995) < 1e-6

@@ -44,6 +44,16 @@ __device__ __forceinline__ typename Vec<T>::type vzero() {
   return v;
 }
 
+// Unconditional load + select: `ok ? *p : 0` without a branch around the load.  hipcc turns a
+// per-lane "load or zero" into a branch with its own s_waitcnt vmcnt(0), which serialises every
+// load of an unrolled staging loop; loading from a clamped, always-valid address and selecting
+// afterwards keeps all loads in flight together.  `safe` must be a readable address.
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type vload_sel(const T* p, const T* safe, bool ok) {
+  typename Vec<T>::type v = vload(ok ? p : safe);
+  return ok ? v : vzero<T>();
+}
+
 // Load/store VEC elements as fp32.
 template <typename T, int N>
 __device__ __forceinline__ void load_f(const T* p, float* o) {
@@ -109,9 +119,15 @@ __device__ __forceinline__ void store_f(float* p, const float* v) {
 // ---- activations (fp32) ---------------------------------------------------------------------
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// SiLU in the conv epilogues: hardware exp2 + reciprocal (v_exp_f32 / v_rcp_f32, ~1 ulp each)
+// instead of the IEEE expf + division sequence; 4-5 VALU ops per element, within the fp32
+// parity tolerance and far below fp16 rounding.
+__device__ __forceinline__ float silu_fast(float v) {
+  return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
+}
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
-    case YDBL_ACT_SILU: return v / (1.0f + expf(-v));
+    case YDBL_ACT_SILU: return silu_fast(v);
     case YDBL_ACT_GELU: return gelu_erf(v);
     case YDBL_ACT_SIGMOID: return sigmoidf_(v);
     default: return v;

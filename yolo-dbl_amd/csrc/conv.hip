@@ -40,6 +40,67 @@ __device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& 
   return c;
 }
 
+// Epilogue of one wave's TN x TM accumulator tiles: lane owns output channels co[i]..co[i]+3 of
+// pixel pp[j].  Every load is unconditional from a clamped address (bias once; the residual of a
+// pixel for all TN tiles at once) so the loads overlap; only the stores are predicated.
+template <typename T, int TN, int TM>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 (&acc)[TN][TM],
+                                              const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN]) {
+  const bool c4 = (p.Cout & 3) == 0;  // uniform: co..co+3 in range whenever co < Cout
+  float bv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    if (p.bias) {
+      if (c4) {
+        load_f<4>(p.bias + min(co[i], p.Cout - 4), bv[i]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[i][q] = p.bias[min(co[i] + q, p.Cout - 1)];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int64_t pc = pv[j] ? pp[j] : 0;
+    float rv[TN][4];
+    if (p.res != YDBL_RES_NONE) {
+      const T* rp = p.r + pc * p.rcs;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        if (c4) {
+          load_f<4>(rp + min(co[i], p.Cout - 4), rv[i]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rv[i][q] = float(rp[min(co[i] + q, p.Cout - 1)]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[i][j][q] + bv[i][q], p.act);
+      if (p.res == YDBL_RES_ADD) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = rv[i][q] + v[q];
+      } else if (p.res == YDBL_RES_MUL) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = rv[i][q] * v[q];
+      }
+      if (!pv[j] || co[i] >= p.Cout) continue;
+      T* yp = p.y + pc * p.ycs + co[i];
+      if (co[i] + 4 <= p.Cout) {
+        store_f<4>(yp, v);
+      } else {
+        for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) yp[q] = (T)v[q];
+      }
+    }
+  }
+}
+
 // LDS-staged implicit GEMM.  Workgroup tile = BM output pixels x BN output channels, 4 waves as
 // WM x WN, each wave TM x TN MFMA tiles of 16x16.  K (= taps x Cin, tap-major, NHWC-contiguous
 // within a tap) advances in steps of BK = four 16-byte vectors per row (32 f16 / 16 f32):
@@ -98,28 +159,42 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
     bix[it] = ox * p.S - p.PAD;
   }
   vec ra[A_IT], rb[B_IT];
+  // k-walk state: every staging vector of this thread has k-vector tid&3, so one (ky, kx, ci)
+  // cursor serves all of them; it advances by BK per step with no integer division.
+  int cur_ci = (tid & 3) * VEC, cur_kx = 0, cur_ky = 0;
+  if constexpr (!POINTWISE) {
+    const int tap = cur_ci / p.Cin;
+    cur_ci -= tap * p.Cin;
+    cur_ky = tap / p.KW;
+    cur_kx = tap - cur_ky * p.KW;
+  }
+  auto advance = [&]() {
+    if constexpr (!POINTWISE) {
+      cur_ci += BK;
+      while (cur_ci >= p.Cin) {
+        cur_ci -= p.Cin;
+        if (++cur_kx == p.KW) { cur_kx = 0; ++cur_ky; }
+      }
+    }
+  };
   auto load_step = [&](int ks) {
+    // every load is unconditional (clamped address) and masked afterwards: no branch per load
 #pragma unroll
-    for (int it = 0; it < A_IT; ++it) ra[it] = aval[it] ? vload(arow[it] + ks * BK) : vzero<T>();
+    for (int it = 0; it < A_IT; ++it) ra[it] = vload_sel(arow[it] + ks * BK, p.w, aval[it]);
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int v = tid + it * 256;
       const int k = ks * BK + (v & 3) * VEC;
-      vec val = vzero<T>();
-      if (bval[it] && k < p.K) {
-        if constexpr (POINTWISE) {
-          val = vload(p.x + bpix[it] * p.xcs + k);
-        } else {
-          const int tap = k / p.Cin;
-          const int ci = k - tap * p.Cin;
-          const int ky = tap / p.KW, kx = tap - ky * p.KW;
-          const int iy = biy[it] + ky * p.DIL, ix = bix[it] + kx * p.DIL;
-          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
-            val = vload(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + ci);
-        }
+      const bool kin = k < p.K;
+      if constexpr (POINTWISE) {
+        rb[it] = vload_sel(p.x + bpix[it] * p.xcs + k, p.x, bval[it] && kin);
+      } else {
+        const int iy = biy[it] + cur_ky * p.DIL, ix = bix[it] + cur_kx * p.DIL;
+        const bool ok = bval[it] && kin && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        rb[it] = vload_sel(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + cur_ci, p.x, ok);
       }
-      rb[it] = val;
     }
+    advance();
   };
   auto store_step = [&](int buf) {
 #pragma unroll
@@ -160,43 +235,18 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane owns channels co..co+3 of pixel pp
+  // ---- epilogue
+  int64_t pp[TM];
+  bool pv[TM];
+  int co[TN];
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
-    const int64_t pp = m0 + wm * TM * 16 + j * 16 + r16;
-    if (pp >= p.P) continue;
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int co = n0 + wn * TN * 16 + i * 16 + 4 * g;
-      if (co >= p.Cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      const bool full = co + 4 <= p.Cout;
-      if (p.bias) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] += (full || co + q < p.Cout) ? p.bias[co + q] : 0.f;
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act);
-      if (p.res != YDBL_RES_NONE) {
-        float rv[4];
-        const T* rp = p.r + pp * p.rcs + co;
-        if (full) {
-          load_f<4>(rp, rv);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rv[q] = (co + q < p.Cout) ? float(rp[q]) : 0.f;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = (p.res == YDBL_RES_ADD) ? rv[q] + v[q] : rv[q] * v[q];
-      }
-      T* yp = p.y + pp * p.ycs + co;
-      if (full) {
-        store_f<4>(yp, v);
-      } else {
-        for (int q = 0; q < 4 && co + q < p.Cout; ++q) yp[q] = (T)v[q];
-      }
-    }
+    pp[j] = m0 + wm * TM * 16 + j * 16 + r16;
+    pv[j] = pp[j] < p.P;
   }
+#pragma unroll
+  for (int i = 0; i < TN; ++i) co[i] = n0 + wn * TN * 16 + i * 16 + 4 * g;
+  conv_epilogue<T, TN, TM>(p, acc, pp, pv, co);
 }
 
 // Spatial-tile 3x3 conv for thin inputs (Cin <= 32, the high-resolution backbone layers).
@@ -240,12 +290,11 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
       vec t[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int i = base + u * 256 + tid;
+        const int i = min(base + u * 256 + tid, TOT - 1);
         const int pix = i / CV, cv = i - pix * CV;
         const int iy = iy0 + pix / IW, ix = ix0 + pix % IW;
-        t[u] = (i < TOT && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
-                   ? vload(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + cv * VEC)
-                   : vzero<T>();
+        const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        t[u] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + cv * VEC, p.x, ok);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -258,9 +307,9 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
       vec t[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int i = base + u * 256 + tid;
+        const int i = min(base + u * 256 + tid, WTOT - 1);
         const int co = i / (KPAD / VEC), kv = i % (KPAD / VEC);
-        t[u] = (i < WTOT && co < p.Cout) ? vload(p.w + (int64_t)co * p.KPAD + kv * VEC) : vzero<T>();
+        t[u] = vload_sel(p.w + (int64_t)co * p.KPAD + kv * VEC, p.w, co < p.Cout);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -303,32 +352,19 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
       for (int j = 0; j < TM; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
   }
 
+  int64_t pp[TM];
+  bool pv[TM];
+  int co[NTN];
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     const int op = wave * TM * 16 + j * 16 + r16;
     const int oy = oy0 + op / TW, ox = ox0 + op % TW;
-    if (oy >= p.Ho || ox >= p.Wo) continue;
-    const int64_t pp = ((int64_t)b * p.Ho + oy) * p.Wo + ox;
-#pragma unroll
-    for (int i = 0; i < NTN; ++i) {
-      const int co = i * 16 + 4 * g;
-      if (co >= p.Cout) continue;
-      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
-      if (p.bias) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] += p.bias[co + q];
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act);
-      if (p.res != YDBL_RES_NONE) {
-        float rv[4];
-        load_f<4>(p.r + pp * p.rcs + co, rv);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = (p.res == YDBL_RES_ADD) ? rv[q] + v[q] : rv[q] * v[q];
-      }
-      store_f<4>(p.y + pp * p.ycs + co, v);
-    }
+    pv[j] = oy < p.Ho && ox < p.Wo;
+    pp[j] = ((int64_t)b * p.Ho + oy) * p.Wo + ox;
   }
+#pragma unroll
+  for (int i = 0; i < NTN; ++i) co[i] = i * 16 + 4 * g;
+  conv_epilogue<T, NTN, TM>(p, acc, pp, pv, co);
 }
 
 template <typename T, int CIN, int S, int TH, int TW, int NTN>

@@ -86,11 +86,11 @@ __global__ __launch_bounds__(256) void dwconv_lds_kernel(DView<const T> x, DView
     vec tmp[IT];
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
-      const int i = threadIdx.x + it * 256;
+      const int i = min((int)threadIdx.x + it * 256, TOT - 1);
       const int cv = i % CV, px = i / CV;
       const int iy = iy0 + px / IW, ix = ix0 + px % IW;
-      tmp[it] = (i < TOT && iy >= 0 && iy < x.h && ix >= 0 && ix < x.w) ? vload(x.at(b, iy, ix) + c0 + cv * V)
-                                                                       : vzero<T>();
+      const bool ok = iy >= 0 && iy < x.h && ix >= 0 && ix < x.w;
+      tmp[it] = vload_sel(x.at(b, iy, ix) + c0 + cv * V, x.p + c0, ok);
     }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {

@@ -27,31 +27,36 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
                                                    int act, DView<T> y) {
   extern __shared__ __align__(16) unsigned char smem[];
   T* tile = reinterpret_cast<T*>(smem);  // [rows_in][cin][wpad]
-  const int rows_in = (STEM_ROWS - 1) * S + 3;
   const int wpad = W + 2;
   const int b = blockIdx.y;
   const int oy0 = blockIdx.x * STEM_ROWS;
   const int iy0 = oy0 * S - 1;
-  // stage: every element of the tile is one independent 4-byte load; batches of 8 per thread are
-  // issued before any is stored so the loads overlap instead of serialising on their latency.
-  const int total = rows_in * cin * wpad;
-  for (int base = 0; base < total; base += 256 * 8) {
-    float v[8];
+  // stage: for each of the ROWS_IN x 3 input lines, threads cover the padded row in 256-wide
+  // chunks; the loads of all lines of a chunk are issued before any store (no integer division,
+  // clamped addresses, zero padding by select).
+  constexpr int ROWS_IN = (STEM_ROWS - 1) * S + 3;
+  for (int x0 = 0; x0 < wpad; x0 += 256) {
+    const int xx = x0 + threadIdx.x;
+    const int ix = xx - 1;
+    const bool okx = xx < wpad && ix >= 0 && ix < W;
+    const int ixc = min(max(ix, 0), W - 1);
+    float v[ROWS_IN][3];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = base + u * 256 + threadIdx.x;
-      v[u] = 0.f;
-      if (i < total) {
-        const int line = i / wpad, xx = i - line * wpad;
-        const int r = line / cin, c = line - r * cin;
-        const int iy = iy0 + r, ix = xx - 1;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v[u] = x[(((int64_t)b * cin + c) * H + iy) * W + ix] * scale;
+    for (int r = 0; r < ROWS_IN; ++r) {
+      const int iy = iy0 + r;
+      const bool ok = okx && iy >= 0 && iy < H;
+      const int iyc = min(max(iy, 0), H - 1);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float t = x[(((int64_t)b * 3 + c) * H + iyc) * W + ixc];
+        v[r][c] = ok ? t * scale : 0.f;
       }
     }
+    if (xx < wpad) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = base + u * 256 + threadIdx.x;
-      if (i < total) tile[i] = T(v[u]);
+      for (int r = 0; r < ROWS_IN; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) tile[(r * 3 + c) * wpad + xx] = T(v[r][c]);
     }
   }
   __syncthreads();
@@ -70,9 +75,15 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const int co = 16 * t + r16;
-      afrag[t][j] = (k < K && co < y.c) ? float(T(wt[(co * cin + c) * 9 + ky * 3 + kx])) : 0.f;
+      const float wv = wt[(min(co, y.c - 1) * cin + c) * 9 + ky * 3 + kx];  // unconditional, then select
+      afrag[t][j] = (k < K && co < y.c) ? float(T(wv)) : 0.f;
     }
   }
+  float bv[NT][4];  // bias of this lane's output channels, loaded once
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bv[t][q] = bias[min(16 * t + 4 * g + q, y.c - 1)];
   const int Wo = y.w;
   const int tiles_per_row = (Wo + 15) / 16;
   for (int tt = wave; tt < STEM_ROWS * tiles_per_row; tt += 4) {
@@ -112,7 +123,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
       if (co >= y.c) continue;
       float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[t][q] + bias[co + q], act);
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[t][q] + bv[t][q], act);
       store_f<4>(yp + co, v);
     }
   }
@@ -127,7 +138,7 @@ extern "C" int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h,
                               const ydbl_view* y, void* stream) {
   if (!x || !wt || !bias) return fail(YDBL_EINVAL, "stem: null input/weights");
   if (check_view(y, "stem.y", true)) return YDBL_EINVAL;
-  if (cin < 1 || cin > 3) return fail(YDBL_EINVAL, "stem: cin must be 1..3 (K = 9*cin <= 32)");
+  if (cin != 3) return fail(YDBL_EINVAL, "stem: cin must be 3 (RGB; K = 27 = one MFMA k-step)");
   if (k != 3 || (stride != 1 && stride != 2)) return fail(YDBL_EINVAL, "stem: k=3, stride 1 or 2 only");
   const int ho = (h + 2 * (k / 2) - k) / stride + 1, wo = (w + 2 * (k / 2) - k) / stride + 1;
   if (y->n != n || y->h != ho || y->w != wo) return fail(YDBL_EINVAL, "stem: output shape mismatch");

@@ -126,7 +126,7 @@ def stem_ok(m, ch: int) -> bool:
     if type(m) is not Conv:
         return False
     c = m.conv
-    return (c.groups == 1 and c.in_channels == ch and 1 <= ch <= 3 and c.kernel_size == (3, 3)
+    return (c.groups == 1 and c.in_channels == ch and ch == 3 and c.kernel_size == (3, 3)
             and c.padding == (1, 1) and c.dilation == (1, 1) and c.stride[0] == c.stride[1] in (1, 2)
             and c.out_channels % 4 == 0 and c.out_channels <= 64 and isinstance(m.act, (nn.SiLU, nn.Identity)))
 
