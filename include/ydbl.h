@@ -21,6 +21,7 @@
  *   ydbl_conv2d_nhwc       <- nn/modules/conv.py:39-63 Conv.forward_fuse (conv+bias+SiLU after
  *                             nn/tasks.py:207-235 fuse), conv.py:91-108 DSConv pointwise+BN+SiLU,
  *                             nn.Conv2d 1x1 in Detect/LSKblock/DySample, nn.Linear in AdaHG
+ *   ydbl_dsconv_nhwc       <- DSConv.forward conv.py:91-108 (dw + pw + BN + SiLU, one kernel)
  *   ydbl_dwconv2d_nhwc     <- depthwise nn.Conv2d (DSConv.dw conv.py:98, DWConv conv.py:128-133,
  *                             GhostConv.cv2 conv.py:194, LSKblock.conv0/conv_spatial LSKA.py:31-32)
  *   ydbl_input_nchw_to_nhwc<- BasePredictor.preprocess engine/predictor.py:116-134 (+ LoadTensor /255)
@@ -75,6 +76,20 @@ typedef struct {
   int32_t act, res_mode;
 } ydbl_conv_desc;
 int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream);
+
+/* DSConv in one kernel (conv.py:91-108): y = act(pw(dw(x)) + bias) [+ r], BN folded into pw.
+ * dw_w fp32 [k*k][cin] (no dw bias), pw_w [cout][kpad] in the view dtype (kpad = round_up(cin, 32),
+ * zero padded), bias fp32 [cout].  cin multiple of 32 (f16) / 16 (f32).  The depthwise output is
+ * rounded to the view dtype (the reference's intermediate tensor) and never leaves LDS. */
+typedef struct {
+  ydbl_view x, y, r;
+  const float* dw_w;
+  const void* pw_w;
+  const float* bias;
+  int32_t k, stride, pad, dil;
+  int32_t kpad, act, res_mode;
+} ydbl_dsconv_desc;
+int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 
 /* Depthwise convolution (groups = C), fp32 arithmetic.
  * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).

@@ -35,6 +35,7 @@ STRUCTS = {
     "ydbl_view": "View",
     "ydbl_conv_desc": "ConvDesc",
     "ydbl_dwconv_desc": "DwConvDesc",
+    "ydbl_dsconv_desc": "DsConvDesc",
     "ydbl_hg_desc": "HgDesc",
     "ydbl_decode_desc": "DecodeDesc",
     "ydbl_pred_cand_desc": "PredCandDesc",

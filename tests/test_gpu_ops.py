@@ -47,6 +47,9 @@ def _tol(dtype):
     (8, 16, 3, 1, "silu", None), (16, 32, 3, 2, "silu", None), (64, 64, 3, 1, "silu", "add"),
     (24, 80, 1, 1, "none", None), (128, 3, 1, 1, "none", None), (32, 48, 1, 1, "silu", "mul"),
     (96, 144, 3, 2, "silu", None), (8, 8, 3, 1, "silu", None),
+    # K >= 512: wave-split-K kernel (1x1 and 3x3, Cout tails, residual add/mul)
+    (512, 96, 1, 1, "silu", "add"), (128, 200, 3, 1, "silu", None), (72, 22, 3, 1, "none", "mul"),
+    (256, 32, 3, 1, "silu", None), (64, 128, 3, 2, "silu", None),
 ])
 def test_conv_dense(dtype, cin, cout, k, s, act, res):
     from ydbl import _lib
@@ -228,6 +231,31 @@ def test_hyperace(dtype):
     xs = [torch.randn(2, 64, 16, 16), torch.randn(2, 64, 8, 8), torch.randn(2, 128, 4, 4)]
     tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
     _module_parity(o, M.HyperACE(*args), xs, dtype, tol, multi=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin,cout,k,s,shape", [
+    (64, 64, 3, 1, (2, 64, 20, 19)), (64, 64, 7, 1, (2, 64, 17, 23)), (128, 128, 3, 2, (2, 128, 20, 20)),
+    (128, 256, 3, 2, (1, 128, 18, 18)), (32, 32, 7, 1, (3, 32, 9, 13)), (64, 48, 5, 1, (2, 64, 11, 12)),
+])
+def test_dsconv_fused(dtype, cin, cout, k, s, shape):
+    """DSConv (dw -> pw -> BN -> SiLU) through the single-kernel ydbl_dsconv_nhwc path vs the oracle module."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(cin + cout + k)
+    o = om.DSConv(cin, cout, k, s).eval()
+    with torch.no_grad():
+        for bn in [m for m in o.modules() if isinstance(m, torch.nn.BatchNorm2d)]:
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 2.0)
+            bn.weight.uniform_(0.5, 1.5)
+    x = torch.randn(*shape)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    p_mod = M.DSConv(cin, cout, k, s)
+    plan = _plan(dtype)
+    assert M.fused_dsconv_ok(p_mod.dw, _tv_from_nchw(plan, x), dtype)
+    _module_parity(o, p_mod, [x], dtype, tol)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])

@@ -9,97 +9,9 @@
 // f32 -> four exact-f32 v_mfma_f32_16x16x4_f32 (parity mode; same fmaf-chain numerics as VALU).
 // Fused epilogue: + bias, activation (SiLU/GELU/sigmoid), residual add or multiply, write into a
 // channel slice of a wider buffer (concat without copies).
-#include "common.hpp"
+#include "conv_common.hpp"
 
 namespace ydbl {
-
-template <typename T>
-struct ConvArgs {
-  const T* x; int xcs; int N, H, W, Cin;
-  T* y; int ycs; int Ho, Wo, Cout;
-  const T* r; int rcs;
-  const T* w; const float* bias;
-  int KW, S, PAD, DIL, K, KPAD;
-  int act, res;
-  int P;
-};
-
-template <typename T>
-__device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a, const typename Vec<T>::type& b, f32x4 c);
-
-template <>
-__device__ __forceinline__ f32x4 mfma_chunk<_Float16>(const h8& a, const h8& b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-}
-template <>
-__device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
-  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
-  return c;
-}
-
-// Epilogue of one wave's TN x TM accumulator tiles: lane owns output channels co[i]..co[i]+3 of
-// pixel pp[j].  Every load is unconditional from a clamped address (bias once; the residual of a
-// pixel for all TN tiles at once) so the loads overlap; only the stores are predicated.
-template <typename T, int TN, int TM>
-__device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 (&acc)[TN][TM],
-                                              const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN]) {
-  const bool c4 = (p.Cout & 3) == 0;  // uniform: co..co+3 in range whenever co < Cout
-  float bv[TN][4];
-#pragma unroll
-  for (int i = 0; i < TN; ++i) {
-    if (p.bias) {
-      if (c4) {
-        load_f<4>(p.bias + min(co[i], p.Cout - 4), bv[i]);
-      } else {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) bv[i][q] = p.bias[min(co[i] + q, p.Cout - 1)];
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int64_t pc = pv[j] ? pp[j] : 0;
-    float rv[TN][4];
-    if (p.res != YDBL_RES_NONE) {
-      const T* rp = p.r + pc * p.rcs;
-#pragma unroll
-      for (int i = 0; i < TN; ++i) {
-        if (c4) {
-          load_f<4>(rp + min(co[i], p.Cout - 4), rv[i]);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) rv[i][q] = float(rp[min(co[i] + q, p.Cout - 1)]);
-        }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[i][j][q] + bv[i][q], p.act);
-      if (p.res == YDBL_RES_ADD) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = rv[i][q] + v[q];
-      } else if (p.res == YDBL_RES_MUL) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = rv[i][q] * v[q];
-      }
-      if (!pv[j] || co[i] >= p.Cout) continue;
-      T* yp = p.y + pc * p.ycs + co[i];
-      if (co[i] + 4 <= p.Cout) {
-        store_f<4>(yp, v);
-      } else {
-        for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) yp[q] = (T)v[q];
-      }
-    }
-  }
-}
 
 // LDS-staged implicit GEMM.  Workgroup tile = BM output pixels x BN output channels, 4 waves as
 // WM x WN, each wave TM x TN MFMA tiles of 16x16.  K (= taps x Cin, tap-major, NHWC-contiguous
@@ -405,6 +317,188 @@ static bool try_tile(const ConvArgs<T>& a, int kh, hipStream_t s) {
   }
 }
 
+// Wave-split-K implicit GEMM for large K (3x3 with Cin >= 64, wide 1x1): every wave computes the
+// whole BM x BN tile (TM x TN = up to 16 MFMA tiles) over its quarter of each 4*BK-deep k-block,
+// so a barrier is amortised over TM*TN MFMAs per wave instead of (TM*TN)/4; the four partial
+// tiles are summed through LDS in fixed wave order before the fused epilogue.
+// LDS rows are 16 vectors (4*BK elements), slot-swizzled with (kv ^ row) so both the staging
+// stores and the 16x16 fragment reads are bank-conflict-free.
+template <typename T, int BM, int BN, bool POINTWISE>
+__global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
+  constexpr int VEC = Vec<T>::N;
+  constexpr int BK = 4 * VEC;    // per wave
+  constexpr int BKB = 4 * BK;    // per block step
+  constexpr int TM = BM / 16, TN = BN / 16;
+  constexpr int A_IT = BN * 16 / 256, B_IT = BM * 16 / 256;
+  static_assert(A_IT >= 1 && B_IT >= 1, "tile");
+  using vec = typename Vec<T>::type;
+  constexpr int STAGE = 2 * (BN + BM) * 16;          // vectors, double-buffered
+  constexpr int RED = 4 * TN * TM * 64;              // f32x4 partials (16 B each = one vec)
+  __shared__ vec smem[STAGE > RED ? STAGE : RED];
+  vec* sA = smem;                                     // [2][BN*16]
+  vec* sB = smem + 2 * BN * 16;                       // [2][BM*16]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int kv = tid & 15;  // every staging vector of this thread has k-vector kv
+
+  const T* arow[A_IT];
+  bool aval[A_IT];
+#pragma unroll
+  for (int it = 0; it < A_IT; ++it) {
+    const int co = n0 + ((tid + it * 256) >> 4);
+    aval[it] = co < p.Cout;
+    arow[it] = p.w + (int64_t)(aval[it] ? co : 0) * p.KPAD + kv * VEC;
+  }
+  int bb[B_IT], biy[B_IT], bix[B_IT];
+  int64_t bpix[B_IT];
+  bool bval[B_IT];
+#pragma unroll
+  for (int it = 0; it < B_IT; ++it) {
+    int pp = m0 + ((tid + it * 256) >> 4);
+    bval[it] = pp < p.P;
+    pp = bval[it] ? pp : 0;
+    bpix[it] = pp;
+    const int ox = pp % p.Wo;
+    const int t = pp / p.Wo;
+    bb[it] = t / p.Ho;
+    biy[it] = (t % p.Ho) * p.S - p.PAD;
+    bix[it] = ox * p.S - p.PAD;
+  }
+  int cur_ci = kv * VEC, cur_kx = 0, cur_ky = 0;
+  if constexpr (!POINTWISE) {
+    const int tap = cur_ci / p.Cin;
+    cur_ci -= tap * p.Cin;
+    cur_ky = tap / p.KW;
+    cur_kx = tap - cur_ky * p.KW;
+  }
+  vec ra[A_IT], rb[B_IT];
+  auto load_step = [&](int kb) {
+    const int k = kb * BKB + kv * VEC;
+    const bool kin = k < p.K;
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) ra[it] = vload_sel(arow[it] + kb * BKB, p.w, aval[it] && kin);
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      if constexpr (POINTWISE) {
+        rb[it] = vload_sel(p.x + bpix[it] * p.xcs + k, p.x, bval[it] && kin);
+      } else {
+        const int iy = biy[it] + cur_ky * p.DIL, ix = bix[it] + cur_kx * p.DIL;
+        const bool ok = bval[it] && kin && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        rb[it] = vload_sel(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + cur_ci, p.x, ok);
+      }
+    }
+    if constexpr (!POINTWISE) {
+      cur_ci += BKB;
+      while (cur_ci >= p.Cin) {
+        cur_ci -= p.Cin;
+        if (++cur_kx == p.KW) { cur_kx = 0; ++cur_ky; }
+      }
+    }
+  };
+  auto store_step = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < A_IT; ++it) {
+      const int row = (tid + it * 256) >> 4;
+      sA[buf * BN * 16 + row * 16 + (kv ^ (row & 15))] = ra[it];
+    }
+#pragma unroll
+    for (int it = 0; it < B_IT; ++it) {
+      const int row = (tid + it * 256) >> 4;
+      sB[buf * BM * 16 + row * 16 + (kv ^ (row & 15))] = rb[it];
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nsteps = (p.K + BKB - 1) / BKB;
+  load_step(0);
+  store_step(0);
+  __syncthreads();
+  const int myk = wave * 4 + g;  // k-vector this lane reads inside a block step
+  for (int kb = 0; kb < nsteps; ++kb) {
+    const int buf = kb & 1;
+    if (kb + 1 < nsteps) load_step(kb + 1);
+    vec af[TN], bf[TM];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int row = i * 16 + r16;
+      af[i] = sA[buf * BN * 16 + row * 16 + (myk ^ (row & 15))];
+    }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int row = j * 16 + r16;
+      bf[j] = sB[buf * BM * 16 + row * 16 + (myk ^ (row & 15))];
+    }
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+    if (kb + 1 < nsteps) store_step(buf ^ 1);
+    __syncthreads();
+  }
+
+  // cross-wave reduction: partial tile (i, j) of wave w at red[((w * TN + i) * TM + j) * 64 + lane]
+  f32x4* red = reinterpret_cast<f32x4*>(smem);
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) red[((wave * TN + i) * TM + j) * 64 + lane] = acc[i][j];
+  __syncthreads();
+  for (int t = wave; t < TN * TM; t += 4) {
+    const int i = t / TM, j = t % TM;
+    f32x4 sum = red[((0 * TN + i) * TM + j) * 64 + lane];
+#pragma unroll
+    for (int w = 1; w < 4; ++w) {
+      const f32x4 o = red[((w * TN + i) * TM + j) * 64 + lane];
+      sum = f32x4{sum[0] + o[0], sum[1] + o[1], sum[2] + o[2], sum[3] + o[3]};
+    }
+    const f32x4 one[1][1] = {{sum}};
+    const int64_t pp[1] = {m0 + j * 16 + r16};
+    const bool pv[1] = {pp[0] < p.P};
+    const int co[1] = {n0 + i * 16 + 4 * g};
+    conv_epilogue<T, 1, 1>(p, one, pp, pv, co);
+  }
+}
+
+template <typename T, int BM, int BN>
+static void launch_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
+  if (pointwise)
+    conv_wsk_kernel<T, BM, BN, true><<<grid, 256, 0, s>>>(a);
+  else
+    conv_wsk_kernel<T, BM, BN, false><<<grid, 256, 0, s>>>(a);
+}
+
+// Wave-split-K where the block-tiled GEMM runs out of parallelism or k-depth per barrier:
+// K >= 1024, or K >= 512 on small maps (measured on DBL-n: 384->64 3x3 @40^2 112 -> 82 us,
+// 256->64 3x3 @20^2 47 -> 27 us; 64->64 3x3 @80^2 stays on conv_igemm_kernel, 47 vs 74 us).
+template <typename T>
+static bool try_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
+  if (!(a.K >= 1024 || (a.K >= 512 && a.P <= 16384))) return false;
+  auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
+  const int64_t want = 768;
+  if (a.Cout <= 32) {
+    if (blocks(128, 32) >= want) { launch_wsk<T, 128, 32>(a, pointwise, s); return true; }
+    launch_wsk<T, 64, 32>(a, pointwise, s);
+    return true;
+  }
+  if (a.Cout <= 64) {
+    if (blocks(64, 64) >= want) { launch_wsk<T, 64, 64>(a, pointwise, s); return true; }
+    launch_wsk<T, 32, 64>(a, pointwise, s);
+    return true;
+  }
+  if (blocks(32, 128) >= want || a.Cout % 128 == 0) { launch_wsk<T, 32, 128>(a, pointwise, s); return true; }
+  launch_wsk<T, 32, 64>(a, pointwise, s);
+  return true;
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 static void launch_igemm(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
@@ -454,7 +548,7 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   a.act = d->act; a.res = d->res_mode;
   a.P = d->y.n * d->y.h * d->y.w;
   const bool pw = d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->x.h == d->y.h && d->x.w == d->y.w;
-  if (!try_tile<T>(a, d->kh, s)) dispatch_conv<T>(a, pw, s);
+  if (!try_tile<T>(a, d->kh, s) && !try_wsk<T>(a, pw, s)) dispatch_conv<T>(a, pw, s);
   return check_launch("ydbl_conv2d_nhwc");
 }
 

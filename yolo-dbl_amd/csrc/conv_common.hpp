@@ -1,0 +1,96 @@
+// Shared pieces of the MFMA convolution kernels (conv.hip, dsconv.hip): argument block,
+// MFMA k-chunk (f16 16x16x32 / exact f32 4x 16x16x4) and the fused epilogue.
+#pragma once
+#include "common.hpp"
+
+namespace ydbl {
+
+template <typename T>
+struct ConvArgs {
+  const T* x; int xcs; int N, H, W, Cin;
+  T* y; int ycs; int Ho, Wo, Cout;
+  const T* r; int rcs;
+  const T* w; const float* bias;
+  int KW, S, PAD, DIL, K, KPAD;
+  int act, res;
+  int P;
+};
+
+template <typename T>
+__device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a, const typename Vec<T>::type& b, f32x4 c);
+
+template <>
+__device__ __forceinline__ f32x4 mfma_chunk<_Float16>(const h8& a, const h8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& b, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+
+// Epilogue of one wave's TN x TM accumulator tiles: lane owns output channels co[i]..co[i]+3 of
+// pixel pp[j].  Every load is unconditional from a clamped address (bias once; the residual of a
+// pixel for all TN tiles at once) so the loads overlap; only the stores are predicated.
+template <typename T, int TN, int TM>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 (&acc)[TN][TM],
+                                              const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN]) {
+  const bool c4 = (p.Cout & 3) == 0;  // uniform: co..co+3 in range whenever co < Cout
+  float bv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    if (p.bias) {
+      if (c4) {
+        load_f<4>(p.bias + min(co[i], p.Cout - 4), bv[i]);
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bv[i][q] = p.bias[min(co[i] + q, p.Cout - 1)];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int64_t pc = pv[j] ? pp[j] : 0;
+    float rv[TN][4];
+    if (p.res != YDBL_RES_NONE) {
+      const T* rp = p.r + pc * p.rcs;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        if (c4) {
+          load_f<4>(rp + min(co[i], p.Cout - 4), rv[i]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rv[i][q] = float(rp[min(co[i] + q, p.Cout - 1)]);
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[i][j][q] + bv[i][q], p.act);
+      if (p.res == YDBL_RES_ADD) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = rv[i][q] + v[q];
+      } else if (p.res == YDBL_RES_MUL) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = rv[i][q] * v[q];
+      }
+      if (!pv[j] || co[i] >= p.Cout) continue;
+      T* yp = p.y + pc * p.ycs + co[i];
+      if (co[i] + 4 <= p.Cout) {
+        store_f<4>(yp, v);
+      } else {
+        for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) yp[q] = (T)v[q];
+      }
+    }
+  }
+}
+
+}  // namespace ydbl

@@ -38,6 +38,12 @@ class DwConvDesc(C.Structure):
                 ("act", C.c_int32), ("res_mode", C.c_int32)]
 
 
+class DsConvDesc(C.Structure):
+    _fields_ = [("x", View), ("y", View), ("r", View), ("dw_w", C.c_void_p), ("pw_w", C.c_void_p),
+                ("bias", C.c_void_p), ("k", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
+                ("dil", C.c_int32), ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32)]
+
+
 class HgDesc(C.Structure):
     _fields_ = [("x", View), ("xp", View), ("y", View), ("num_edges", C.c_int32), ("num_heads", C.c_int32),
                 ("proto_base", C.c_void_p), ("ctx_w", C.c_void_p), ("ctx_b", C.c_void_p),
@@ -74,6 +80,7 @@ _VP = C.POINTER(View)
 SIGNATURES = {
     "ydbl_conv2d_nhwc": ([C.POINTER(ConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
+    "ydbl_dsconv_nhwc": ([C.POINTER(DsConvDesc), _P], C.c_int),
     "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
     "ydbl_conv_stem": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _P, _P, C.c_int32, C.c_int32,
                         C.c_int32, _VP, _P], C.c_int),

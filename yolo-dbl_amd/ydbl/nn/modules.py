@@ -121,6 +121,32 @@ def emit_conv2d(plan: Plan, conv: nn.Conv2d, x: TV, out: TV | None, weight=None,
     return y
 
 
+def fused_dsconv_ok(dw: nn.Conv2d, x: TV, dtype) -> bool:
+    k, st, d = dw.kernel_size[0], dw.stride[0], dw.dilation[0]
+    cc = 32 if dtype == torch.float16 else 16
+    return (dw.kernel_size[0] == dw.kernel_size[1] and (k, st, d) in ((3, 1, 1), (3, 2, 1), (5, 1, 1), (7, 1, 1))
+            and x.c % cc == 0 and x.c == dw.in_channels)
+
+
+def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Tensor, b_pw: torch.Tensor,
+                act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv") -> TV:
+    """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA."""
+    k, st, p, d = dw.kernel_size[0], dw.stride[0], dw.padding[0], dw.dilation[0]
+    c = x.c
+    co = w_pw.shape[0]
+    ho, wo = conv_out_hw(x.h, x.w, k, st, p, d)
+    y = out if out is not None else plan.alloc(x.n, ho, wo, co)
+    assert (y.h, y.w, y.c) == (ho, wo, co), ((y.h, y.w, y.c), (ho, wo, co))
+    dww = plan.const(dw.weight.detach().float().cpu().reshape(c, k * k).t().contiguous())
+    kpad = round_up(c, 32)
+    pww = plan.const(torch.nn.functional.pad(w_pw.reshape(co, c).float(), (0, kpad - c)).to(plan.dtype))
+    bd = plan.const(b_pw.float())
+    desc = _lib.DsConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(),
+                           dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode)
+    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, desc])
+    return y
+
+
 def stem_ok(m, ch: int) -> bool:
     """The first layer can run as ydbl_conv_stem (3x3 Conv on the raw NCHW image)."""
     if type(m) is not Conv:
@@ -199,8 +225,10 @@ class DSConv(nn.Module):
         self.act = nn.SiLU()
 
     def emit(self, plan, x, out=None, res=None, res_mode=_lib.RES_NONE):
-        t = emit_conv2d(plan, self.dw, x, None, what=f"DSConv.dw{self.dw.kernel_size[0]}")
         w, b = fold_bn(self.pw.weight, self.pw.bias, self.bn)
+        if self.dw.bias is None and fused_dsconv_ok(self.dw, x, plan.dtype):
+            return emit_dsconv(plan, self.dw, x, out, w, b, _lib.ACT_SILU, res, res_mode)
+        t = emit_conv2d(plan, self.dw, x, None, what=f"DSConv.dw{self.dw.kernel_size[0]}")
         return emit_conv2d(plan, self.pw, t, out, w, b, _lib.ACT_SILU, res, res_mode, what="DSConv.pw")
 
 
