@@ -23,7 +23,7 @@ __global__ __launch_bounds__(256) void dsconv_kernel(ConvArgs<T> p, const float*
   constexpr int HIT = (HALO + 255) / 256;
   using vec = typename Vec<T>::type;
   __shared__ vec s_halo[HALO];
-  __shared__ f32x4 s_w[K * K * CC / 4];
+  __shared__ vec s_w[K * K * 4];  // taps in the activation dtype (the reference's .half() weights)
   __shared__ vec s_b[64 * 4];
 
   const int tid = threadIdx.x;
@@ -59,9 +59,14 @@ __global__ __launch_bounds__(256) void dsconv_kernel(ConvArgs<T> p, const float*
         const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         t[it] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + c0 + cv * VEC, p.x, ok);
       }
-      for (int i = tid; i < K * K * CC / 4; i += 256) {
-        const int tap = i / (CC / 4), q = i % (CC / 4);
-        s_w[i] = *reinterpret_cast<const f32x4*>(dww + tap * p.Cin + c0 + 4 * q);
+      for (int i = tid; i < K * K * 4; i += 256) {
+        const int tap = i >> 2, q = i & 3;
+        float wf[VEC];
+        load_f<VEC>(dww + tap * p.Cin + c0 + q * VEC, wf);
+        vec wv;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) wv[e] = T(wf[e]);
+        s_w[i] = wv;
       }
 #pragma unroll
       for (int it = 0; it < HIT; ++it) {
@@ -82,14 +87,9 @@ __global__ __launch_bounds__(256) void dsconv_kernel(ConvArgs<T> p, const float*
           const int ix = dox * S - p.PAD + kx * DIL;
           if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
           const vec xv = s_halo[((dpy * S + ky * DIL) * IW + dpxx * S + kx * DIL) * 4 + dcv];
-          float wv[VEC];
+          const vec wv = s_w[(ky * K + kx) * 4 + dcv];
 #pragma unroll
-          for (int h = 0; h < VEC / 4; ++h) {
-            const f32x4 w4 = s_w[(ky * K + kx) * (CC / 4) + dcv * (VEC / 4) + h];
-            wv[4 * h] = w4[0]; wv[4 * h + 1] = w4[1]; wv[4 * h + 2] = w4[2]; wv[4 * h + 3] = w4[3];
-          }
-#pragma unroll
-          for (int q = 0; q < VEC; ++q) a[q] = fmaf(float(xv[q]), wv[q], a[q]);
+          for (int q = 0; q < VEC; ++q) a[q] = fmaf(float(xv[q]), float(wv[q]), a[q]);  // fp32 accumulate
         }
       }
       vec o;
