@@ -1,0 +1,51 @@
+"""Micro-benchmark of ydbl_conv2d_nhwc on the DBL-n 3x3 / 1x1 shapes (HIP-event timed, fp16, bs 32).
+
+    YDBL_NO_HALO=1 python scripts/conv_bench.py   # implicit-GEMM kernels only, for A/B
+"""
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "yolo-dbl_amd"))
+import torch  # noqa: E402
+
+from ydbl.nn import modules as M  # noqa: E402
+from ydbl.runtime import Plan  # noqa: E402
+
+SHAPES = [  # (cin, cout, k, s, H)
+    (384, 64, 3, 1, 40), (64, 128, 3, 1, 40), (256, 32, 3, 1, 80), (64, 64, 3, 2, 80), (192, 64, 3, 1, 40),
+    (128, 128, 3, 2, 40), (64, 64, 3, 1, 80), (128, 64, 3, 1, 40), (64, 64, 3, 1, 40), (256, 64, 3, 1, 20),
+    (64, 64, 3, 1, 20), (64, 32, 3, 1, 80),
+    (64, 128, 1, 1, 80), (128, 64, 1, 1, 80), (64, 64, 1, 1, 80), (64, 64, 1, 1, 40), (128, 128, 1, 1, 40),
+    (384, 128, 1, 1, 40), (512, 128, 1, 1, 40), (128, 64, 1, 1, 40), (384, 256, 1, 1, 20), (64, 3, 1, 1, 80),
+]
+
+
+def bench(plan, reps=20):
+    plan.run()
+    torch.cuda.synchronize()
+    torch.cuda._sleep(int(5e7))
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        plan.run()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+B = 32
+sel = [int(a) for a in sys.argv[1:]]
+for idx, (ci, co, k, s, H) in enumerate(SHAPES):
+    if sel and idx not in sel:
+        continue
+    plan = Plan(torch.device("cuda"), torch.float16)
+    x = plan.alloc(B, H, H, ci)
+    x.torch().copy_(torch.randn(B, H, H, ci, dtype=torch.float16))
+    m = M.Conv(ci, co, k, s).eval()
+    m.emit(plan, x)
+    t = bench(plan)
+    ho = H // s
+    mb = (B * H * H * ci + B * ho * ho * co + co * ci * k * k) * 2 / 1e6
+    tf = 2.0 * B * ho * ho * co * ci * k * k / 1e12
+    print(f"{ci:4d}->{co:4d} k{k} s{s} @{H:3d}: {t:7.1f} us  {mb / t:6.2f} TB/s  {tf / t * 1e6:7.1f} TF", flush=True)

@@ -115,6 +115,40 @@ def test_conv_tile(dtype, cin, cout, s, h, w, res):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("n,cin,cout,h,w,res", [
+    (2, 64, 32, 161, 163, None),      # ragged 8x16 tiles on both edges, Cout 32 (NTN 2)
+    (2, 128, 64, 160, 160, "add"),    # residual add (Bottleneck), one 64-channel split
+    (1, 64, 128, 200, 256, None),     # 4-row tiles (few workgroups), two output-channel splits
+    (2, 256, 48, 170, 152, "add"),    # deepest Cin the halo path takes, Cout not a multiple of 16
+])
+def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
+    """3x3 stride-1 convs with 64 <= Cin <= 256 on >= 51200 output pixels: the halo-tiled kernel."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + cout + h)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 1, 1))
+    assert n * h * w >= 51200
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+    ybuf = plan.alloc(n, h, w, cout + 8)
+    yv = ybuf.cslice(8, cout)
+    rv, mode = None, _lib.RES_NONE
+    if res:
+        r = torch.randn(n, cout, h, w)
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD
+        ref = r.to(dtype).float() + ref
+    emit_dense(plan, xv, yv, wt, b, 1, 1, 1, _lib.ACT_SILU, rv, mode)
+    _run(plan)
+    tol = _tol(dtype) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("c,k,s,d,bias,res", [(16, 3, 1, 1, False, False), (32, 3, 2, 1, True, False),
                                              (64, 7, 1, 1, False, True), (24, 5, 1, 1, True, False),
                                              (16, 7, 1, 3, True, False), (16, 3, 1, 2, False, False),
@@ -237,6 +271,10 @@ def test_hyperace(dtype):
 @pytest.mark.parametrize("cin,cout,k,s,shape", [
     (64, 64, 3, 1, (2, 64, 20, 19)), (64, 64, 7, 1, (2, 64, 17, 23)), (128, 128, 3, 2, (2, 128, 20, 20)),
     (128, 256, 3, 2, (1, 128, 18, 18)), (32, 32, 7, 1, (3, 32, 9, 13)), (64, 48, 5, 1, (2, 64, 11, 12)),
+    # whole-row tiles: 40-wide (TH 4) and 20-wide (TH 8) outputs, ragged last row band, XCD remap
+    (64, 64, 7, 1, (2, 64, 14, 40)), (64, 64, 3, 1, (2, 64, 40, 40)), (128, 128, 3, 2, (2, 128, 18, 80)),
+    (128, 256, 3, 2, (2, 128, 40, 40)), (32, 32, 7, 1, (2, 32, 20, 20)), (128, 128, 7, 1, (1, 128, 20, 20)),
+    (128, 128, 3, 1, (4, 128, 128, 80)),  # Cout 128 in one workgroup (NTN 8)
 ])
 def test_dsconv_fused(dtype, cin, cout, k, s, shape):
     """DSConv (dw -> pw -> BN -> SiLU) through the single-kernel ydbl_dsconv_nhwc path vs the oracle module."""

@@ -44,6 +44,27 @@ __device__ __forceinline__ typename Vec<T>::type vzero() {
   return v;
 }
 
+// ---- 8-byte half vector of T (4 x f16 or 2 x f32): the depthwise phases' channel group --------
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+template <typename T> struct HVec;
+template <> struct HVec<_Float16> {
+  static constexpr int N = 4;
+  using type = h4;
+};
+template <> struct HVec<float> {
+  static constexpr int N = 2;
+  using type = f32x2;
+};
+
+// XCD-aware block order.  Workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD
+// b % 8), each with its own L2; remapping so that XCD x walks the contiguous logical range
+// [x*n/8, (x+1)*n/8) keeps neighbouring tiles (shared halo rows, shared input tile of several
+// output-channel splits) in one L2.  Identity when n is not a multiple of 8.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  if (n & 7) return b;
+  return (b & 7) * (n >> 3) + (b >> 3);
+}
+
 // Unconditional load + select: `ok ? *p : 0` without a branch around the load.  hipcc turns a
 // per-lane "load or zero" into a branch with its own s_waitcnt vmcnt(0), which serialises every
 // load of an unrolled staging loop; loading from a clamped, always-valid address and selecting

@@ -9,6 +9,8 @@
 // f32 -> four exact-f32 v_mfma_f32_16x16x4_f32 (parity mode; same fmaf-chain numerics as VALU).
 // Fused epilogue: + bias, activation (SiLU/GELU/sigmoid), residual add or multiply, write into a
 // channel slice of a wider buffer (concat without copies).
+#include <stdlib.h>
+
 #include "conv_common.hpp"
 
 namespace ydbl {
@@ -548,7 +550,9 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   a.act = d->act; a.res = d->res_mode;
   a.P = d->y.n * d->y.h * d->y.w;
   const bool pw = d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->x.h == d->y.h && d->x.w == d->y.w;
-  if (!try_tile<T>(a, d->kh, s) && !try_wsk<T>(a, pw, s)) dispatch_conv<T>(a, pw, s);
+  static const bool no_halo = getenv("YDBL_NO_HALO") != nullptr;  // A/B switch for scripts/conv_bench.py
+  if (!try_tile<T>(a, d->kh, s) && (no_halo || !try_conv3x3_halo<T>(a, d->kh, s)) && !try_wsk<T>(a, pw, s))
+    dispatch_conv<T>(a, pw, s);
   return check_launch("ydbl_conv2d_nhwc");
 }
 

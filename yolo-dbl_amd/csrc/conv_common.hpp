@@ -16,6 +16,10 @@ struct ConvArgs {
   int P;
 };
 
+// conv3x3.hip: halo-tiled 3x3 kernel for Cin >= 2 k-steps; false when the shape is not its own.
+template <typename T>
+bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s);
+
 template <typename T>
 __device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a, const typename Vec<T>::type& b, f32x4 c);
 

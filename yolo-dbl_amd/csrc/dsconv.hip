@@ -1,134 +1,227 @@
 // DSConv fused into one kernel (U/nn/modules/conv.py:91-108: SiLU(BN(pw1x1(dw_kxk(x))))), BN
-// folded into the pointwise weights.  The depthwise output never touches HBM:
-//   for each 4-vector channel chunk of Cin (32 f16 / 16 f32 = one MFMA k-step of the pointwise):
-//     1. stage the chunk's input halo tile and depthwise taps in LDS,
-//     2. 256 threads = 64 tile pixels x 4 channel vectors compute the depthwise outputs (fp32
-//        accumulate in the reference's tap order, padded taps skipped), round to the activation
-//        dtype (the reference's fp16 dw output) and write them as the MFMA B tile [64 px][k],
-//     3. wave w multiplies its 16 pixels by the chunk's pointwise weights (A fragments straight
-//        from the L2-resident [Cout][KPAD] matrix) into NTN 16x16 accumulators.
+// folded into the pointwise weights.  The depthwise output never touches HBM.
+//
+// A workgroup owns a TH x TW output tile and NTN*16 output channels.  For each chunk of
+// CC = 4*VEC input channels (= one MFMA k-step of the pointwise):
+//   1. the chunk's input halo tile and depthwise taps sit in LDS as fp32 (converted once per
+//      element at staging; the next chunk's halo is loaded into registers before this chunk's
+//      arithmetic and stored after it, into a second buffer or the refilled single one),
+//   2. depthwise phase: a thread owns CSEG consecutive outputs of one row and one fp32 quad of
+//      channels; it slides a (CSEG-1)*S + K register window along each input row, so every LDS
+//      element it reads feeds up to K outputs (fp32 accumulate in the reference's (ky, kx) tap
+//      order; padded taps read staged zeros, fma(0, w, a) == a), rounds to the activation dtype
+//      (the reference's fp16 dw output) and writes the MFMA B tile [TH*TW px][CC],
+//   3. pointwise phase: wave w multiplies its 16-pixel tiles w, w+4, ... by the chunk's
+//      pointwise weights (A fragments loaded from the L2-resident [Cout][KPAD] matrix at the top
+//      of the chunk) into NTN x TMW 16x16 accumulators.
 // Fused epilogue (bias, SiLU, residual add of DSBottleneck, channel-slice store) as conv.hip.
 #include "conv_common.hpp"
 
 namespace ydbl {
 
-template <typename T, int K, int S, int DIL, int NTN>
-__global__ __launch_bounds__(256) void dsconv_kernel(ConvArgs<T> p, const float* __restrict__ dww, int tiles_x,
-                                                     int tiles_y) {
+template <int R>
+__device__ __forceinline__ int bswz(int row, int kv) {  // B-tile slot: 16 consecutive rows -> distinct banks
+  return row * 4 + (kv ^ (((row >> 2) & 1) << 1));
+}
+
+// 4 consecutive activation-dtype channels from 4 fp32 values (8 B f16 / 16 B f32).
+__device__ __forceinline__ void store4(_Float16* d, const float* a) {
+  *reinterpret_cast<h4*>(d) = h4{(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3]};
+}
+__device__ __forceinline__ void store4(float* d, const float* a) {
+  *reinterpret_cast<f32x4*>(d) = f32x4{a[0], a[1], a[2], a[3]};
+}
+
+template <typename T, int K, int S, int DIL, int TH, int TW, int CSEG, int NTN, bool DBUF>
+__global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const float* __restrict__ dww, int tiles_x,
+                                                        int tiles_y, int co_splits) {
   constexpr int VEC = Vec<T>::N;
-  constexpr int CC = 4 * VEC;  // channels per chunk = one MFMA k-step
-  constexpr int TH = 8, TW = 8;
+  constexpr int CC = 4 * VEC;    // channels per chunk (one pointwise MFMA k-step)
+  constexpr int NQ = CC / 4;     // fp32 quads per staged pixel
+  constexpr int QV = VEC / 4;    // quads per 16-byte activation vector
   constexpr int IH = (TH - 1) * S + (K - 1) * DIL + 1, IW = (TW - 1) * S + (K - 1) * DIL + 1;
-  constexpr int HALO = IH * IW * 4;  // vectors
+  constexpr int IWP = IW | 1;    // odd row pitch: the rows of a half-wave hit distinct bank quarters
+  constexpr int NSEG = TW / CSEG;
+  static_assert(TW % CSEG == 0, "segments");
+  constexpr int NTASK = NQ * TH * NSEG;  // (quad, row, segment), quad fastest
+  constexpr int SEGW = (CSEG - 1) * S + (K - 1) * DIL + 1;
+  constexpr int HALO = IH * IW * 4;      // 16-byte activation vectors to stage per chunk
   constexpr int HIT = (HALO + 255) / 256;
+  constexpr int NT = TH * TW / 16;       // 16-pixel MFMA tiles
+  static_assert(TH * TW % 16 == 0, "tile");
+  constexpr int TMW = (NT + 3) / 4;
   using vec = typename Vec<T>::type;
-  __shared__ vec s_halo[HALO];
-  __shared__ vec s_w[K * K * 4];  // taps in the activation dtype (the reference's .half() weights)
-  __shared__ vec s_b[64 * 4];
+  // the halo and the taps are staged as fp32 (converted once per element, not once per tap use)
+  constexpr int NB = DBUF ? 2 : 1;  // double-buffered halo, or one buffer refilled between barriers
+  __shared__ f32x4 s_x[NB][IH * IWP * NQ];
+  __shared__ f32x4 s_w[NB][K * K * NQ];
+  __shared__ vec s_b[TH * TW * 4];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  int bid = blockIdx.x;
+  const int ntiles = p.N * tiles_y * tiles_x;
+  int bid = xcd_remap(blockIdx.x, ntiles * co_splits);
+  const int cs = bid % co_splits;
+  bid /= co_splits;
   const int tx = bid % tiles_x; bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int b = bid / tiles_y;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - p.PAD, ix0 = ox0 * S - p.PAD;
-  const int co0 = blockIdx.y * NTN * 16;
+  const int co0 = cs * NTN * 16;
 
-  // dw-phase role: pixel dpx of the tile, channel vector dcv of the chunk
-  const int dpx = tid >> 2, dcv = tid & 3;
-  const int dpy = dpx / TW, dpxx = dpx % TW;
-  const int doy = oy0 + dpy, dox = ox0 + dpxx;
-
-  f32x4 acc[NTN][1];
+  constexpr int TAPV = K * K * NQ;  // fp32 tap quads per chunk (392 for k7 f16: > one per thread)
+  constexpr int TIT = (TAPV + 255) / 256;
+  vec xr[HIT];
+  f32x4 wr[TIT];
+  auto load_chunk = [&](int c0) {
 #pragma unroll
-  for (int i = 0; i < NTN; ++i) acc[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < HIT; ++it) {
+      const int i = min(tid + it * 256, HALO - 1);
+      const int cv = i & 3, px = i >> 2;
+      const int hy = px / IW, hx = px - hy * IW;
+      const int iy = iy0 + hy, ix = ix0 + hx;
+      const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      xr[it] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + c0 + cv * VEC, p.x, ok);
+    }
+#pragma unroll
+    for (int it = 0; it < TIT; ++it) {  // taps rounded to the activation dtype (the reference's .half() weights)
+      const int i = min(tid + it * 256, TAPV - 1);
+      const int tap = i / NQ, q = i % NQ;
+      const f32x4 w = *reinterpret_cast<const f32x4*>(dww + tap * p.Cin + c0 + q * 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) wr[it][e] = float(T(w[e]));
+    }
+  };
+  auto store_chunk = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < HIT; ++it) {
+      const int i = tid + it * 256;
+      if (i < HALO) {
+        const int cv = i & 3, px = i >> 2;
+        const int hy = px / IW, hx = px - hy * IW;
+        f32x4* d = &s_x[buf][(hy * IWP + hx) * NQ + cv * QV];
+#pragma unroll
+        for (int u = 0; u < QV; ++u)
+          d[u] = f32x4{float(xr[it][4 * u]), float(xr[it][4 * u + 1]), float(xr[it][4 * u + 2]), float(xr[it][4 * u + 3])};
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < TIT; ++it)
+      if (tid + it * 256 < TAPV) s_w[buf][tid + it * 256] = wr[it];
+  };
+
+  f32x4 acc[NTN][TMW];
+#pragma unroll
+  for (int i = 0; i < NTN; ++i)
+#pragma unroll
+    for (int j = 0; j < TMW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nchunks = p.Cin / CC;
+  load_chunk(0);
+  store_chunk(0);
+  __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
+    const int buf = DBUF ? (ch & 1) : 0;
     const int c0 = ch * CC;
-    {  // 1. stage halo (all loads in flight, then stores) and the chunk's depthwise taps
-      vec t[HIT];
+    if (ch + 1 < nchunks) load_chunk(c0 + CC);
+    vec af[NTN];
 #pragma unroll
-      for (int it = 0; it < HIT; ++it) {
-        const int i = min(tid + it * 256, HALO - 1);
-        const int cv = i & 3, px = i >> 2;
-        const int iy = iy0 + px / IW, ix = ix0 + px % IW;
-        const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        t[it] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + c0 + cv * VEC, p.x, ok);
-      }
-      for (int i = tid; i < K * K * 4; i += 256) {
-        const int tap = i >> 2, q = i & 3;
-        float wf[VEC];
-        load_f<VEC>(dww + tap * p.Cin + c0 + q * VEC, wf);
-        vec wv;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) wv[e] = T(wf[e]);
-        s_w[i] = wv;
-      }
-#pragma unroll
-      for (int it = 0; it < HIT; ++it) {
-        const int i = tid + it * 256;
-        if (i < HALO) s_halo[i] = t[it];
-      }
+    for (int i = 0; i < NTN; ++i) {
+      const int co = co0 + i * 16 + r16;
+      af[i] = vload_sel(p.w + (int64_t)co * p.KPAD + c0 + g * VEC, p.w, co < p.Cout);
     }
-    __syncthreads();
-    {  // 2. depthwise outputs of this chunk -> B tile
-      float a[VEC];
+    // ---- depthwise phase
+    for (int task = tid; task < NTASK; task += 256) {
+      const int q = task % NQ;
+      const int r = (task / NQ) % TH;
+      const int sg = task / (NQ * TH);
+      float a[CSEG][4];
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) a[q] = 0.f;
+      for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[c][e] = 0.f;
 #pragma unroll 1
-      for (int ky = 0; ky < K; ++ky) {
-        const int iy = doy * S - p.PAD + ky * DIL;
+      for (int ky = 0; ky < K; ++ky) {  // rolled: one input row's window + taps live at a time
+        const f32x4* xrow = &s_x[buf][((r * S + ky * DIL) * IWP + sg * CSEG * S) * NQ + q];
+        f32x4 xs[SEGW], wv[K];
 #pragma unroll
-        for (int kx = 0; kx < K; ++kx) {
-          const int ix = dox * S - p.PAD + kx * DIL;
-          if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.W) continue;
-          const vec xv = s_halo[((dpy * S + ky * DIL) * IW + dpxx * S + kx * DIL) * 4 + dcv];
-          const vec wv = s_w[(ky * K + kx) * 4 + dcv];
+        for (int i = 0; i < SEGW; ++i) xs[i] = xrow[i * NQ];
 #pragma unroll
-          for (int q = 0; q < VEC; ++q) a[q] = fmaf(float(xv[q]), float(wv[q]), a[q]);  // fp32 accumulate
-        }
+        for (int kx = 0; kx < K; ++kx) wv[kx] = s_w[buf][(ky * K + kx) * NQ + q];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+          for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[c][e] = fmaf(xs[c * S + kx * DIL][e], wv[kx][e], a[c][e]);
       }
-      vec o;
 #pragma unroll
-      for (int q = 0; q < VEC; ++q) o[q] = T(a[q]);
-      s_b[dpx * 4 + (dcv ^ (((dpx >> 2) & 1) << 1))] = o;
+      for (int c = 0; c < CSEG; ++c) {
+        const int px = r * TW + sg * CSEG + c;
+        store4(reinterpret_cast<T*>(&s_b[bswz<0>(px, q / QV)]) + (q % QV) * 4, a[c]);
+      }
     }
     __syncthreads();
-    {  // 3. pointwise MFMA: wave's 16 pixels x NTN*16 output channels, one k-step
-      const int row = wave * 16 + r16;
-      const vec bf = s_b[row * 4 + (g ^ (((row >> 2) & 1) << 1))];
+    // ---- pointwise phase
 #pragma unroll
-      for (int i = 0; i < NTN; ++i) {
-        const int co = co0 + i * 16 + r16;
-        const vec af = vload_sel(p.w + (int64_t)co * p.KPAD + c0 + g * VEC, p.w, co < p.Cout);
-        acc[i][0] = mfma_chunk<T>(af, bf, acc[i][0]);
+    for (int j = 0; j < TMW; ++j) {
+      const int t = wave + 4 * j;
+      if (t < NT) {
+        const vec bf = s_b[bswz<0>(t * 16 + r16, g)];
+#pragma unroll
+        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_chunk<T>(af[i], bf, acc[i][j]);
+      }
+    }
+    if constexpr (DBUF) {
+      if (ch + 1 < nchunks) store_chunk(buf ^ 1);
+    } else {
+      if (ch + 1 < nchunks) {
+        __syncthreads();  // every wave is past this chunk's depthwise reads
+        store_chunk(0);
       }
     }
     __syncthreads();
   }
-  const int op = wave * 16 + r16;
-  const int oy = oy0 + op / TW, ox = ox0 + op % TW;
-  const bool pv[1] = {oy < p.Ho && ox < p.Wo};
-  const int64_t pp[1] = {((int64_t)b * p.Ho + oy) * p.Wo + ox};
+
+  int64_t pp[TMW];
+  bool pv[TMW];
+#pragma unroll
+  for (int j = 0; j < TMW; ++j) {
+    const int t = wave + 4 * j;
+    const int op = t * 16 + r16;
+    const int oy = oy0 + op / TW, ox = ox0 + op % TW;
+    pv[j] = t < NT && oy < p.Ho && ox < p.Wo;
+    pp[j] = ((int64_t)b * p.Ho + oy) * p.Wo + ox;
+  }
   int co[NTN];
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
-  conv_epilogue<T, NTN, 1>(p, acc, pp, pv, co);
+  conv_epilogue<T, NTN, TMW>(p, acc, pp, pv, co);
 }
 
+template <typename T, int K, int S, int DIL, int TH, int TW, int CSEG, bool DBUF = true>
+static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, hipStream_t s) {
+  const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
+  const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
+  auto go = [&](auto kern, int ntn) {
+    const int cs = (int)cdiv(a.Cout, ntn * 16);
+    kern<<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, dww, tiles_x, tiles_y, cs);
+  };
+  if (a.Cout <= 32) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
+  else if (a.Cout <= 64 || ntiles < 256) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
+  else go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 8, DBUF>, 8);
+}
+
+// Tile shape (measured on the DBL-n/s shapes, fp16 bs 32): maps wider than 20 px take a 16x8 tile
+// with 4-output row segments and one refilled LDS buffer (small footprint: 3-4 workgroups per CU
+// hide each other's halo loads; 40^2 k7 64ch 25.8 -> 15.1 us); 20-px and smaller maps take an 8x8
+// double-buffered tile (more workgroups on the few pixels).
 template <typename T, int K, int S, int DIL>
 static int launch_ds(const ConvArgs<T>& a, const float* dww, hipStream_t s) {
-  const int tiles_x = (int)cdiv(a.Wo, 8), tiles_y = (int)cdiv(a.Ho, 8);
-  const unsigned gx = (unsigned)(a.N * tiles_y * tiles_x);
-  if (a.Cout <= 32) {
-    dsconv_kernel<T, K, S, DIL, 2><<<dim3(gx, 1), 256, 0, s>>>(a, dww, tiles_x, tiles_y);
-  } else {
-    dsconv_kernel<T, K, S, DIL, 4><<<dim3(gx, (unsigned)cdiv(a.Cout, 64)), 256, 0, s>>>(a, dww, tiles_x, tiles_y);
-  }
+  if (a.Wo > 20) launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, s);
+  else launch_ds_tile<T, K, S, DIL, 8, 8, 2, true>(a, dww, s);
   return check_launch("ydbl_dsconv_nhwc");
 }
 
