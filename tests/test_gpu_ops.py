@@ -178,7 +178,8 @@ def test_dwconv(dtype, c, k, s, d, bias, res):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
-@pytest.mark.parametrize("cout,s,h,w", [(8, 1, 14, 19), (16, 2, 16, 22), (32, 1, 9, 40), (64, 2, 7, 33)])
+@pytest.mark.parametrize("cout,s,h,w", [(8, 1, 14, 19), (16, 2, 16, 22), (32, 1, 9, 40), (64, 2, 7, 33),
+                                          (8, 1, 21, 64), (16, 2, 17, 36), (16, 1, 6, 1280)])
 def test_stem(dtype, cout, s, h, w):
     """ydbl_conv_stem (preprocess + first Conv) vs conv2d on the dtype-rounded image."""
     from ydbl import _lib
