@@ -18,7 +18,9 @@ namespace ydbl {
 // Token slices: image b's N tokens are split into NS slices so that B*NS workgroups fill the chip;
 // every reduction over N writes per-slice partials that the next stage combines in fixed order.
 static int hg_splits(int B, int N) {
-  int ns = (2048 + B - 1) / B;
+  // ~256 workgroups: enough to fill the chip, few enough partials that every combine (proto,
+  // edge) reads at most a few dozen of them per value
+  int ns = (256 + B - 1) / B;
   const int max_ns = (N + 31) / 32;
   if (ns > max_ns) ns = max_ns;
   return ns < 1 ? 1 : ns;
@@ -209,35 +211,31 @@ __global__ __launch_bounds__(HG_LOGIT_TOK) void hg_logits_kernel(DView<const T> 
   }
 }
 
-// softmax over N from the logits partials: (max, 1/sum) per (image, hyperedge)
-template <int E>
-__device__ __forceinline__ void combine_stats(const float* __restrict__ lstat, int b, int nl, float* mx, float* inv) {
-#pragma unroll
-  for (int e = 0; e < E; ++e) {
-    float m = -INFINITY;
-    for (int k = 0; k < nl; ++k) m = fmaxf(m, lstat[(((int64_t)b * nl + k) * E + e) * 2]);
-    float sum = 0.f;
-    for (int k = 0; k < nl; ++k) {
-      const float* st = lstat + (((int64_t)b * nl + k) * E + e) * 2;
-      sum += st[1] * expf(st[0] - m);
-    }
-    mx[e] = m;
-    inv[e] = 1.0f / sum;
-  }
-}
-
-// partial He[b][k][e][d] = sum_{n in slice k} A[n][e] * X[n][d]
+// partial He[b][k][e][d] = sum_{n in slice k} A[n][e] * X[n][d].  The softmax weights A[n][e] of a
+// 64-token chunk are computed once into LDS (not once per channel-vector thread).
+constexpr int HG_CHUNK = 64;
 template <typename T, int E>
 __global__ __launch_bounds__(256) void hg_gather_kernel(DView<const T> x, const float* __restrict__ logits,
                                                         const float* __restrict__ lstat, int nl,
                                                         float* __restrict__ hep, int ns) {
   constexpr int V = Vec<T>::N;
   __shared__ float s_mx[E], s_inv[E];
+  __shared__ float s_a[HG_CHUNK][E];
   __shared__ float red[256][V];
   const int b = blockIdx.y, k = blockIdx.x;
   const int N = x.h * x.w, D = x.c;
-  if (threadIdx.x == 0) combine_stats<E>(lstat, b, nl, s_mx, s_inv);
-  __syncthreads();
+  if (threadIdx.x < E) {
+    const int e = threadIdx.x;
+    float m = -INFINITY;
+    for (int j = 0; j < nl; ++j) m = fmaxf(m, lstat[(((int64_t)b * nl + j) * E + e) * 2]);
+    float sum = 0.f;
+    for (int j = 0; j < nl; ++j) {
+      const float* st = lstat + (((int64_t)b * nl + j) * E + e) * 2;
+      sum += st[1] * expf(st[0] - m);
+    }
+    s_mx[e] = m;
+    s_inv[e] = 1.0f / sum;
+  }
   const int ncv = D / V;
   const int lanes = 256 / ncv;
   const int cv = threadIdx.x % ncv, tl = threadIdx.x / ncv;
@@ -247,23 +245,33 @@ __global__ __launch_bounds__(256) void hg_gather_kernel(DView<const T> x, const 
   for (int e = 0; e < E; ++e)
 #pragma unroll
     for (int q = 0; q < V; ++q) acc[e][q] = 0.f;
-  if (tl < lanes) {
-    const T* xb = x.p + (int64_t)b * N * x.cs + cv * V;
-    const float* l = logits + (int64_t)b * N * E;
-    for (int n = n0 + tl; n < n1; n += lanes) {
-      float xv[V];
-      load_f<V>(xb + (int64_t)n * x.cs, xv);
+  const T* xb = x.p + (int64_t)b * N * x.cs + cv * V;
+  const float* l = logits + (int64_t)b * N * E;
+  for (int c0 = n0; c0 < n1; c0 += HG_CHUNK) {
+    const int cn = min(HG_CHUNK, n1 - c0);
+    __syncthreads();  // s_mx/s_inv ready; previous chunk's s_a consumed
+    for (int i = threadIdx.x; i < cn * E; i += 256) {
+      const int t = i / E, e = i - t * E;
+      s_a[t][e] = expf(l[(int64_t)(c0 + t) * E + e] - s_mx[e]) * s_inv[e];
+    }
+    __syncthreads();
+    if (tl < lanes) {
+      for (int t = tl; t < cn; t += lanes) {
+        float xv[V];
+        load_f<V>(xb + (int64_t)(c0 + t) * x.cs, xv);
 #pragma unroll
-      for (int e = 0; e < E; ++e) {
-        const float a = expf(l[(int64_t)n * E + e] - s_mx[e]) * s_inv[e];
+        for (int e = 0; e < E; ++e) {
+          const float a = s_a[t][e];
 #pragma unroll
-        for (int q = 0; q < V; ++q) acc[e][q] = fmaf(a, xv[q], acc[e][q]);
+          for (int q = 0; q < V; ++q) acc[e][q] = fmaf(a, xv[q], acc[e][q]);
+        }
       }
     }
   }
   float* o = hep + ((int64_t)b * ns + k) * E * D;
 #pragma unroll
   for (int e = 0; e < E; ++e) {
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < V; ++q) red[threadIdx.x][q] = acc[e][q];
     __syncthreads();
@@ -277,17 +285,51 @@ __global__ __launch_bounds__(256) void hg_gather_kernel(DView<const T> x, const 
 #pragma unroll
       for (int q = 0; q < V; ++q) o[e * D + cv * V + q] = v[q];
     }
-    __syncthreads();
   }
 }
 
-// He2 = GELU(He @ We^T + be); He3 = He2 @ Wn^T   (per image, E rows)
+// He2 = GELU(He @ We^T + be); He3 = He2 @ Wn^T   (per image, E rows).  1024 threads per image:
+// a wave owns output rows d, its lanes stride the coalesced weight row d[k] and the E dot
+// products are reduced across the wave.
+constexpr int HG_EDGE_THREADS = 1024;
 template <int E>
-__global__ __launch_bounds__(256) void hg_edge_kernel(const float* __restrict__ hep, int ns,
-                                                      const float* __restrict__ lstat, int nl,
-                                                      float* __restrict__ stats, const float* __restrict__ we,
-                                                      const float* __restrict__ be, const float* __restrict__ wn,
-                                                      float* __restrict__ he3, int D) {
+__device__ __forceinline__ void hg_rows(const float* __restrict__ in, const float* __restrict__ w, int D,
+                                        float* out, const float* __restrict__ bias, bool gelu, float* gout,
+                                        int64_t gstride) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int NW = HG_EDGE_THREADS / 64;
+  for (int d = wave; d < D; d += NW) {
+    const float* wr = w + (int64_t)d * D;
+    float s[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) s[e] = 0.f;
+    for (int k = lane; k < D; k += 64) {
+      const float wv = wr[k];
+#pragma unroll
+      for (int e = 0; e < E; ++e) s[e] = fmaf(in[e * D + k], wv, s[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) s[e] += __shfl_xor(s[e], off, 64);
+    if (lane < E) {
+      float v = s[0];
+#pragma unroll
+      for (int e = 1; e < E; ++e) v = lane == e ? s[e] : v;
+      if (gelu) v = gelu_erf(v + bias[d]);
+      if (out) out[lane * D + d] = v;
+      if (gout) gout[lane * gstride + d] = v;
+    }
+  }
+}
+
+template <int E>
+__global__ __launch_bounds__(HG_EDGE_THREADS) void hg_edge_kernel(const float* __restrict__ hep, int ns,
+                                                                  const float* __restrict__ lstat, int nl,
+                                                                  float* __restrict__ stats, const float* __restrict__ we,
+                                                                  const float* __restrict__ be,
+                                                                  const float* __restrict__ wn,
+                                                                  float* __restrict__ he3, int D) {
   extern __shared__ float sm[];  // he [E][D], he2 [E][D]
   float* sh = sm;
   float* sh2 = sm + E * D;
@@ -298,71 +340,59 @@ __global__ __launch_bounds__(256) void hg_edge_kernel(const float* __restrict__ 
     for (int k = 1; k < ns; ++k) v += p[(int64_t)k * E * D];
     sh[i] = v;
   }
-  if (threadIdx.x == 0) {
-    float mx[E], inv[E];
-    combine_stats<E>(lstat, b, nl, mx, inv);
-    for (int e = 0; e < E; ++e) {
-      stats[((int64_t)b * E + e) * 2] = mx[e];
-      stats[((int64_t)b * E + e) * 2 + 1] = inv[e];
+  if (threadIdx.x < E) {
+    const int e = threadIdx.x;
+    float m = -INFINITY;
+    for (int j = 0; j < nl; ++j) m = fmaxf(m, lstat[(((int64_t)b * nl + j) * E + e) * 2]);
+    float sum = 0.f;
+    for (int j = 0; j < nl; ++j) {
+      const float* st = lstat + (((int64_t)b * nl + j) * E + e) * 2;
+      sum += st[1] * expf(st[0] - m);
     }
+    stats[((int64_t)b * E + e) * 2] = m;
+    stats[((int64_t)b * E + e) * 2 + 1] = 1.0f / sum;
   }
   __syncthreads();
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    const float* wr = we + (int64_t)d * D;
-    float s[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float wv = wr[k];
-#pragma unroll
-      for (int e = 0; e < E; ++e) s[e] = fmaf(sh[e * D + k], wv, s[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < E; ++e) sh2[e * D + d] = gelu_erf(s[e] + be[d]);
-  }
+  hg_rows<E>(sh, we, D, sh2, be, true, nullptr, 0);
   __syncthreads();
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    const float* wr = wn + (int64_t)d * D;
-    float s[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) s[e] = 0.f;
-    for (int k = 0; k < D; ++k) {
-      const float wv = wr[k];
-#pragma unroll
-      for (int e = 0; e < E; ++e) s[e] = fmaf(sh2[e * D + k], wv, s[e]);
-    }
-#pragma unroll
-    for (int e = 0; e < E; ++e) he3[((int64_t)b * E + e) * D + d] = s[e];
-  }
+  hg_rows<E>(sh2, wn, D, nullptr, nullptr, false, he3 + (int64_t)b * E * D, D);
 }
 
+// y[n] = GELU(A[n] @ He3 + bn) + X[n].  A workgroup takes HG_CHUNK tokens of one image: He3[b] and
+// the chunk's softmax weights are staged in LDS once, then threads sweep (token, channel vector).
 template <typename T, int E>
 __global__ __launch_bounds__(256) void hg_out_kernel(DView<const T> x, const float* __restrict__ logits,
                                                      const float* __restrict__ stats, const float* __restrict__ he3,
                                                      const float* __restrict__ bn, DView<T> y) {
   constexpr int V = Vec<T>::N;
+  extern __shared__ float s_he[];  // [E][D]
+  __shared__ float s_a[HG_CHUNK][E];
   const int D = x.c, N = x.h * x.w;
-  const int cg = D / V;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)x.n * N * cg) return;
-  const int d0 = (int)(idx % cg) * V;
-  const int64_t tok = idx / cg;
-  const int b = (int)(tok / N);
-  float a[E];
-  const float* l = logits + tok * E;
-#pragma unroll
-  for (int e = 0; e < E; ++e)
-    a[e] = expf(l[e] - stats[((int64_t)b * E + e) * 2]) * stats[((int64_t)b * E + e) * 2 + 1];
-  float xv[V], o[V];
-  load_f<V>(x.pix(tok) + d0, xv);
-#pragma unroll
-  for (int q = 0; q < V; ++q) {
-    float s = 0.f;
-#pragma unroll
-    for (int e = 0; e < E; ++e) s = fmaf(a[e], he3[((int64_t)b * E + e) * D + d0 + q], s);
-    o[q] = gelu_erf(s + bn[d0 + q]) + xv[q];
+  const int b = blockIdx.y;
+  const int c0 = blockIdx.x * HG_CHUNK;
+  const int cn = min(HG_CHUNK, N - c0);
+  for (int i = threadIdx.x; i < E * D; i += 256) s_he[i] = he3[(int64_t)b * E * D + i];
+  for (int i = threadIdx.x; i < cn * E; i += 256) {
+    const int t = i / E, e = i - t * E;
+    const float* st = stats + ((int64_t)b * E + e) * 2;
+    s_a[t][e] = expf(logits[((int64_t)b * N + c0 + t) * E + e] - st[0]) * st[1];
   }
-  store_f<V>(y.pix(tok) + d0, o);
+  __syncthreads();
+  const int cg = D / V;
+  for (int i = threadIdx.x; i < cn * cg; i += 256) {
+    const int t = i / cg, d0 = (i - t * cg) * V;
+    const int64_t tok = (int64_t)b * N + c0 + t;
+    float xv[V], o[V];
+    load_f<V>(x.pix(tok) + d0, xv);
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      float s = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) s = fmaf(s_a[t][e], s_he[e * D + d0 + q], s);
+      o[q] = gelu_erf(s + bn[d0 + q]) + xv[q];
+    }
+    store_f<V>(y.pix(tok) + d0, o);
+  }
 }
 
 template <typename T>
@@ -389,10 +419,9 @@ static int hg_propagate_t(const ydbl_hg_desc* d, hipStream_t s) {
   hg_logits_kernel<T, E><<<dim3(w.nl, B), HG_LOGIT_TOK, E * D * sizeof(float), s>>>(cv<T>(d->xp), w.proto, w.logits,
                                                                                      w.lstat, H, inv_scale);
   hg_gather_kernel<T, E><<<dim3(w.ns, B), 256, 0, s>>>(cv<T>(d->x), w.logits, w.lstat, w.nl, w.hep, w.ns);
-  hg_edge_kernel<E><<<B, 256, 2 * E * D * sizeof(float), s>>>(w.hep, w.ns, w.lstat, w.nl, w.stats, d->edge_w,
-                                                               d->edge_b, d->node_w, w.he3, D);
-  const int V = Vec<T>::N;
-  hg_out_kernel<T, E><<<(unsigned)cdiv((int64_t)B * N * (D / V), 256), 256, 0, s>>>(
+  hg_edge_kernel<E><<<B, HG_EDGE_THREADS, 2 * E * D * sizeof(float), s>>>(
+      w.hep, w.ns, w.lstat, w.nl, w.stats, d->edge_w, d->edge_b, d->node_w, w.he3, D);
+  hg_out_kernel<T, E><<<dim3((unsigned)cdiv(N, HG_CHUNK), B), 256, E * D * sizeof(float), s>>>(
       cv<T>(d->x), w.logits, w.stats, w.he3, d->node_b, dview<T>(d->y));
   return check_launch("ydbl_hg_propagate");
 }
