@@ -43,6 +43,8 @@ def conv_traffic(step, elsize):
     byts = (x.n * x.h * x.w * cin + y.n * y.h * y.w * y.c + y.c * k * cin) * elsize
     if d.res_mode:
         byts += y.n * y.h * y.w * y.c * elsize
+    if d.y2.ptr:  # fused FullPAD: second output written + its other input read
+        byts += 2 * y.n * y.h * y.w * y.c * elsize
     flops = 2.0 * y.n * y.h * y.w * y.c * k * cin
     return byts, flops
 

@@ -74,6 +74,11 @@ typedef struct {
   int32_t kh, kw, stride, pad, dil;
   int32_t kpad;
   int32_t act, res_mode;
+  /* Optional second output, FullPAD_Tunnel (nn/modules/block.py:1954-1956) fused into the layer
+   * that produces one of its inputs: y2 = a2 * v + b2 * r2, v = the value stored to y (rounded to
+   * the view dtype first).  y2.ptr == NULL disables it; y2/r2 have y's shape and dtype. */
+  ydbl_view y2, r2;
+  float a2, b2;
 } ydbl_conv_desc;
 int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream);
 

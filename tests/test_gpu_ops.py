@@ -151,6 +151,43 @@ def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("late", ["x0", "x1"])
+def test_fullpad_fused_into_conv(dtype, late):
+    """FullPAD_Tunnel (block.py:1954-1956) on conv outputs becomes the producing conv's second output:
+    the gate_add launch disappears and y = x0 + gate * x1 is unchanged."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(7)
+    n, c, h, w = 2, 32, 12, 20
+    x = torch.randn(n, 16, h, w)
+    convs = [M.Conv(16, c, 3, 1).eval(), M.Conv(16, c, 1, 1).eval()]
+    refs = [om.Conv(16, c, 3, 1).eval(), om.Conv(16, c, 1, 1).eval()]
+    for cv, rf in zip(convs, refs):
+        with torch.no_grad():
+            rf.bn.running_mean.uniform_(-0.2, 0.2)
+            rf.bn.running_var.uniform_(0.5, 2.0)
+        cv.load_state_dict(rf.state_dict())
+    pad, opad = M.FullPAD_Tunnel(), om.FullPAD_Tunnel()
+    with torch.no_grad():
+        opad.gate.fill_(0.37)
+    pad.load_state_dict(opad.state_dict())
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x)
+    ya, yb = convs[0].emit(plan, xv), convs[1].emit(plan, xv)  # yb is produced last
+    xs = [ya, yb] if late == "x1" else [yb, ya]
+    out = pad.emit(plan, xs)
+    assert not any(st.what == "FullPAD" for st in plan.steps)
+    _run(plan)
+    with torch.no_grad():
+        ra, rb = refs[0](x.to(dtype).float()), refs[1](x.to(dtype).float())
+        ref = opad([ra, rb] if late == "x1" else [rb, ra])
+    tol = _tol(dtype) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(out.nchw().float().cpu(), ref, **tol)
+    torch.testing.assert_close(yb.nchw().float().cpu(), rb, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("c,k,s,d,bias,res", [(16, 3, 1, 1, False, False), (32, 3, 2, 1, True, False),
                                              (64, 7, 1, 1, False, True), (24, 5, 1, 1, True, False),
                                              (16, 7, 1, 3, True, False), (16, 3, 1, 2, False, False),

@@ -538,7 +538,7 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
 
 template <typename T>
 static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
-  ConvArgs<T> a;
+  ConvArgs<T> a{};
   a.x = reinterpret_cast<const T*>(d->x.ptr);
   a.xcs = d->x.cs; a.N = d->x.n; a.H = d->x.h; a.W = d->x.w; a.Cin = d->x.c;
   a.y = reinterpret_cast<T*>(d->y.ptr);
@@ -549,6 +549,9 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   a.K = d->kh * d->kw * d->x.c; a.KPAD = d->kpad;
   a.act = d->act; a.res = d->res_mode;
   a.P = d->y.n * d->y.h * d->y.w;
+  a.y2 = reinterpret_cast<T*>(d->y2.ptr); a.y2cs = d->y2.cs;
+  a.r2 = reinterpret_cast<const T*>(d->r2.ptr); a.r2cs = d->r2.cs;
+  a.a2 = d->a2; a.b2 = d->b2;
   const bool pw = d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->x.h == d->y.h && d->x.w == d->y.w;
   static const bool no_halo = getenv("YDBL_NO_HALO") != nullptr;  // A/B switch for scripts/conv_bench.py
   if (!try_tile<T>(a, d->kh, s) && (no_halo || !try_conv3x3_halo<T>(a, d->kh, s)) && !try_wsk<T>(a, pw, s))
@@ -580,6 +583,13 @@ extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
     if (d->r.cs % 4 || d->r.dtype != d->y.dtype) return fail(YDBL_EINVAL, "conv: residual stride/dtype");
     if (d->r.n != d->y.n || d->r.h != d->y.h || d->r.w != d->y.w || d->r.c < d->y.c)
       return fail(YDBL_EINVAL, "conv: residual shape mismatch");
+  }
+  if (d->y2.ptr) {
+    if (check_view(&d->y2, "conv.y2", false) || check_view(&d->r2, "conv.r2", false)) return YDBL_EINVAL;
+    auto same = [&](const ydbl_view& v) {
+      return v.n == d->y.n && v.h == d->y.h && v.w == d->y.w && v.c == d->y.c && v.dtype == d->y.dtype && v.cs % 4 == 0;
+    };
+    if (!same(d->y2) || !same(d->r2)) return fail(YDBL_EINVAL, "conv: y2/r2 must match y (shape, dtype, cs % 4)");
   }
   const hipStream_t s = as_stream(stream);
   return d->x.dtype == YDBL_F16 ? run_conv<_Float16>(d, s) : run_conv<float>(d, s);

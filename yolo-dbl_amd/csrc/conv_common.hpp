@@ -14,6 +14,9 @@ struct ConvArgs {
   int KW, S, PAD, DIL, K, KPAD;
   int act, res;
   int P;
+  T* y2; int y2cs;  // optional second output y2 = a2 * T(v) + b2 * r2 (fused FullPAD)
+  const T* r2; int r2cs;
+  float a2, b2;
 };
 
 // conv3x3.hip: halo-tiled 3x3 kernel for Cin >= 2 k-steps; false when the shape is not its own.
@@ -92,6 +95,19 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
         store_f<4>(yp, v);
       } else {
         for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) yp[q] = (T)v[q];
+      }
+      if (p.y2) {  // uniform
+        const T* r2p = p.r2 + pc * p.r2cs + co[i];
+        T* y2p = p.y2 + pc * p.y2cs + co[i];
+        if (co[i] + 4 <= p.Cout) {
+          float r2v[4];
+          load_f<4>(r2p, r2v);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) r2v[q] = p.a2 * float(T(v[q])) + p.b2 * r2v[q];
+          store_f<4>(y2p, r2v);
+        } else {
+          for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) y2p[q] = T(p.a2 * float(T(v[q])) + p.b2 * float(r2p[q]));
+        }
       }
     }
   }

@@ -227,7 +227,7 @@ static int launch_ds(const ConvArgs<T>& a, const float* dww, hipStream_t s) {
 
 template <typename T>
 static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
-  ConvArgs<T> a;
+  ConvArgs<T> a{};
   a.x = reinterpret_cast<const T*>(d->x.ptr);
   a.xcs = d->x.cs; a.N = d->x.n; a.H = d->x.h; a.W = d->x.w; a.Cin = d->x.c;
   a.y = reinterpret_cast<T*>(d->y.ptr);

@@ -16,6 +16,8 @@ U/nn/tasks.py:217) is folded into its pointwise conv here.
 
 from __future__ import annotations
 
+import os
+
 import math
 
 import torch
@@ -79,8 +81,10 @@ def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None
     wd = plan.const(wk)
     bd = plan.const(b.float()) if b is not None else None
     d = ConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(), wd.data_ptr(),
-                 bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, kpad, act, res_mode)
+                 bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, kpad, act, res_mode,
+                 _null_view(), _null_view(), 0.0, 0.0)
     plan.launch("ydbl_conv2d_nhwc", d, what=what, keep=[wd, bd, d])
+    plan.note_writer(y, d)
 
 
 def emit_dw(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,
@@ -558,8 +562,22 @@ class FullPAD_Tunnel(nn.Module):  # noqa: N801 (reference name)
     def emit(self, plan, xs, out=None):
         a, b = xs
         y = out if out is not None else plan.alloc(a.n, a.h, a.w, a.c)
-        plan.launch("ydbl_gate_add", a.struct(), b.struct(), float(self.gate.detach().float().cpu()), y.struct(),
-                    what="FullPAD")
+        g = float(self.gate.detach().float().cpu())
+        # Fused into the dense conv that produced the later of the two inputs (its epilogue writes
+        # y = a + g*b as a second output; the other input is complete by then).  Otherwise one
+        # ydbl_gate_add launch.
+        if os.environ.get("YDBL_NO_FUSE_PAD"):  # A/B switch for the benches
+            return self._launch(plan, a, b, g, y)
+        ia, ib = plan.writer_of(a), plan.writer_of(b)
+        if ib is not None and (ia is None or ia[0] < ib[0]) and (ia is not None or plan.made_before(a, ib[0])):
+            return plan.fuse_second_output(ib, y, a, g, 1.0) or self._launch(plan, a, b, g, y)
+        if ia is not None and (ib is None or ib[0] < ia[0]) and (ib is not None or plan.made_before(b, ia[0])):
+            return plan.fuse_second_output(ia, y, b, 1.0, g) or self._launch(plan, a, b, g, y)
+        return self._launch(plan, a, b, g, y)
+
+    @staticmethod
+    def _launch(plan, a, b, g, y):
+        plan.launch("ydbl_gate_add", a.struct(), b.struct(), g, y.struct(), what="FullPAD")
         return y
 
 

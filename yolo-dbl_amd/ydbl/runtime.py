@@ -84,6 +84,7 @@ class Plan:
         self.steps: list[Step] = []
         self.buffers: list[torch.Tensor] = []
         self.bytes_allocated = 0
+        self._writers: dict = {}  # view key -> (step index, ConvDesc) of the dense conv that wrote it
 
     # ---------------------------------------------------------------- memory
     def alloc(self, n: int, h: int, w: int, c: int, dtype: torch.dtype | None = None, cs: int | None = None) -> TV:
@@ -108,6 +109,32 @@ class Plan:
     # ---------------------------------------------------------------- launches
     def launch(self, name: str, *args, what: str = "", keep=()):
         self.steps.append(Step(getattr(lib, name), args, what or name, list(keep)))
+
+    # Producer bookkeeping for epilogue fusion: dense-conv launches register the view they wrote.
+    @staticmethod
+    def _vkey(v: TV):
+        return (v.base.data_ptr(), v.off, v.n, v.h, v.w, v.c, v.cs)
+
+    def note_writer(self, y: TV, desc) -> None:
+        self._writers[self._vkey(y)] = (len(self.steps) - 1, desc)
+
+    def writer_of(self, v: TV):
+        """(step index, ConvDesc) of the dense conv that wrote exactly this view, or None."""
+        return self._writers.get(self._vkey(v))
+
+    def made_before(self, v: TV, step: int) -> bool:
+        """True when v was written by a registered conv launch before `step`."""
+        w = self.writer_of(v)
+        return w is not None and w[0] < step
+
+    def fuse_second_output(self, writer, y2: TV, r2: TV, a2: float, b2: float) -> TV | None:
+        """Give the conv launch `writer` the second output y2 = a2 * y + b2 * r2; None if it has one."""
+        _, d = writer
+        if d.y2.ptr:
+            return None
+        d.y2, d.r2, d.a2, d.b2 = y2.struct(), r2.struct(), float(a2), float(b2)
+        self.steps[writer[0]].keep.append((y2, r2))
+        return y2
 
     def run(self, stream: int | None = None):
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream if stream is None else stream)
