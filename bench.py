@@ -28,7 +28,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3}
+MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3, "fp8": 5000.0}
 CFGS = {"n": ("yolov13n_DBL.yaml", "trained_yolov13n_DBL_nc3.npz"),
         "s": ("yolov13s_DBL.yaml", "trained_yolov13s_DBL_nc3.npz"),
         "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc3.npz")}
@@ -40,7 +40,8 @@ def conv_traffic(step, elsize):
     x, y = d.x, d.y
     cin = x.c
     k = d.kh * d.kw
-    byts = (x.n * x.h * x.w * cin + y.n * y.h * y.w * y.c + y.c * k * cin) * elsize
+    wsize = 1 if d.dq else elsize  # e4m3 weights in fp8 mode
+    byts = (x.n * x.h * x.w * cin + y.n * y.h * y.w * y.c) * elsize + y.c * k * cin * wsize
     if d.res_mode:
         byts += y.n * y.h * y.w * y.c * elsize
     if d.y2.ptr:  # fused FullPAD: second output written + its other input read
@@ -52,7 +53,7 @@ def conv_traffic(step, elsize):
 def roofline(session, dtype_name, reps=3):
     """Per-launch HIP-event timing of one eager forward; dominant kernel = the dense conv."""
     plan = session.plan
-    elsize = 2 if dtype_name == "fp16" else 4
+    elsize = 4 if dtype_name == "fp32" else 2  # activation bytes (fp8 mode keeps fp16 activations)
     best = None
     for _ in range(reps):
         t = plan.run_timed()
@@ -142,6 +143,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--fp32", action="store_true")
+    ap.add_argument("--fp8", action="store_true", help="e4m3 dense-conv operands (BASELINE config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     args = ap.parse_args()
@@ -160,12 +162,14 @@ def main():
 
     cfg, fx = CFGS[args.model]
     half = not args.fp32
-    dtype_name = "fp16" if half else "fp32"
+    dtype_name = "fp8" if args.fp8 else ("fp16" if half else "fp32")
     torch.manual_seed(0)
     model = YOLO(cfg, nc=3)
     load_trained(model.model, ROOT / "tests" / "golden" / fx)
     B, S = args.batch, args.imgsz
-    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev)
+    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=args.fp8)
+    if args.fp8:  # activation scales from a separate synthetic calibration batch
+        sess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
     # synthetic images, different per rank, resident in the session's input buffer (HBM)
     sess.load(blob_images(B, S, seed=1234 + rank).to(dev))
     from ydbl.parallel import gather_detections

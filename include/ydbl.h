@@ -79,6 +79,12 @@ typedef struct {
    * the view dtype first).  y2.ptr == NULL disables it; y2/r2 have y's shape and dtype. */
   ydbl_view y2, r2;
   float a2, b2;
+  /* fp8 operands (f16 activations only): when dq != NULL, w holds OCP e4m3 bytes [cout][kpad]
+   * quantized with per-output-channel scales sw, activations are quantized to e4m3 with
+   * x * qscale (saturated to +-448) as they are staged, and dq[co] = 1 / (sw[co] * qscale)
+   * dequantizes the fp32 accumulator before bias and activation. */
+  const float* dq;
+  float qscale;
 } ydbl_conv_desc;
 int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream);
 

@@ -163,7 +163,7 @@ def _cpu_map50(o, x, labels):
     return m.box.map50
 
 
-@pytest.mark.parametrize("half", [False, True])
+@pytest.mark.parametrize("half", [False, True, "fp8"])
 def test_map50_gpu_vs_cpu_pseudo_gt(golden_dir, half):
     """SURVEY §8d mAP protocol: pseudo ground truth = CPU oracle detections at conf 0.25; GPU and CPU
     paths scored with the same val pipeline; acceptance |mAP50_gpu - mAP50_cpu| <= 0.1."""
@@ -183,8 +183,15 @@ def test_map50_gpu_vs_cpu_pseudo_gt(golden_dir, half):
     batch = {"img": x, "cls": torch.cat([lb[:, 0] for lb in labels]),
              "bboxes": torch.cat([lb[:, 1:] for lb in labels]),
              "batch_idx": torch.cat([torch.full((len(lb),), i) for i, lb in enumerate(labels)])}
-    m_gpu = p.val(data=[batch], half=half).box.map50
+    m_gpu = p.val(data=[batch], half=bool(half), fp8=half == "fp8").box.map50
     m_cpu = _cpu_map50(o, x, labels)
-    print(f"mAP50 pseudo-GT: gpu({'fp16' if half else 'fp32'}) {m_gpu:.4f}  cpu {m_cpu:.4f}")
+    tag = "fp8 e4m3 operands" if half == "fp8" else ("fp16" if half else "fp32")
+    print(f"mAP50 pseudo-GT: gpu({tag}) {m_gpu:.4f}  cpu {m_cpu:.4f}  drop {m_cpu - m_gpu:+.4f}")
+    if half == "fp8":
+        # BASELINE config 5 asks for the drop to be reported, not bounded: e4m3 keeps 3 mantissa bits,
+        # and these synthetic (untrained) weights amplify every perturbation (one fp8 layer alone moves
+        # boxes by ~0.5 px, scripts/fp8_diag.py).  Guard against a broken path, not against the drop.
+        assert m_gpu > 0.3 and m_cpu - m_gpu < 0.5
+        return
     assert abs(m_gpu - m_cpu) <= 0.1
     assert m_cpu > 0.5

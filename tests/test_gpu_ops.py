@@ -150,6 +150,55 @@ def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
 
 
+@pytest.mark.parametrize("cin,cout,k,n,h,w,res", [
+    (64, 64, 3, 2, 160, 160, "add"),  # halo-tiled kernel (>= 51200 px)
+    (96, 40, 3, 2, 19, 23, None),     # block implicit GEMM, Cout tail
+    (128, 128, 1, 2, 24, 40, "add"),  # pointwise GEMM
+    (128, 64, 3, 1, 20, 20, None),    # K = 1152: wave-split-K
+    (512, 96, 1, 2, 10, 10, None),    # K = 512 on a small map: wave-split-K pointwise
+])
+def test_conv_fp8(cin, cout, k, n, h, w, res):
+    """e4m3 operands (BASELINE config 5): GPU fp8 MFMA vs a CPU emulation that applies the same
+    quantization (per-channel weight scale, calibrated per-tensor activation scale, saturation)."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+    from ydbl.quant import E4M3_MAX, e4m3_round, enable_fp8, quantize_weights_e4m3
+
+    torch.manual_seed(cin + cout + k + h)
+    x = torch.randn(n, cin, h, w) * 2.0
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout)
+    plan = _plan(torch.float16)
+    xv = _tv_from_nchw(plan, x)
+    ybuf = plan.alloc(n, h, w, cout + 8)
+    yv = ybuf.cslice(8, cout)
+    rv, mode = None, _lib.RES_NONE
+    r = torch.randn(n, cout, h, w)
+    if res:
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD
+    emit_dense(plan, xv, yv, wt, b, 1, k // 2, 1, _lib.ACT_SILU, rv, mode)
+    assert len(plan.fp8_candidates) == 1
+    assert enable_fp8(plan, plan.run) == 1
+    _run(plan)
+    # CPU emulation of the quantized conv
+    x16 = x.half().float()
+    qs = E4M3_MAX / x16.abs().max().item()
+    xq = e4m3_round(x16 * qs)
+    w2 = wt.permute(0, 2, 3, 1).reshape(cout, -1)
+    wq, sw = quantize_weights_e4m3(w2)
+    wdq = wq.view(torch.float8_e4m3fn).float().reshape(cout, k, k, cin).permute(0, 3, 1, 2)
+    acc = F.conv2d(xq, wdq, None, 1, k // 2) / (sw[None, :, None, None] * qs)
+    ref = F.silu(acc + b[None, :, None, None])
+    if res:
+        ref = r.half().float() + ref
+    got = yv.nchw().float().cpu()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+    # and the quantized conv stays close to the exact one (sanity of the scales)
+    exact = F.silu(F.conv2d(x16, wt, b, 1, k // 2)) + (r.half().float() if res else 0)
+    assert (got - exact).abs().mean().item() < 0.05
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("late", ["x0", "x1"])
 def test_fullpad_fused_into_conv(dtype, late):

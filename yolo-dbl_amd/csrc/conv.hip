@@ -22,12 +22,16 @@ namespace ydbl {
 //   -> fragments (ds_read_b128, XOR-swizzled rows: conflict-free for the 16x16 fragment pattern)
 // A = weights [cout][KPAD] (rows shared by the WM waves of a column), B = im2col rows gathered
 // on the fly (shared by the WN waves of a row); one barrier per k-step.
-template <int R>
-__device__ __forceinline__ int swz(int row, int kv) {  // 16B-slot swizzle within a 64-byte row
-  return row * 4 + (kv ^ (((row >> 2) & 1) << 1));
+// Operand-slot swizzle within a row of 4 slots: 16-byte slots (f16/f32) flip by row bit 2, 8-byte
+// fp8 slots by row bit 3, so the 16x16 fragment reads (ds_read_b128 / ds_read_b64 lane groups)
+// are conflict-free.
+template <bool Q8>
+__device__ __forceinline__ int swz(int row, int kv) {
+  if constexpr (Q8) return row * 4 + (kv ^ (((row >> 3) & 1) << 1));
+  else return row * 4 + (kv ^ (((row >> 2) & 1) << 1));
 }
 
-template <typename T, int BM, int BN, int WM, int WN, bool POINTWISE>
+template <typename T, int BM, int BN, int WM, int WN, bool POINTWISE, bool Q8>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;
@@ -35,8 +39,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile config");
   constexpr int A_IT = (BN * 4 + 255) / 256, B_IT = (BM * 4 + 255) / 256;
   using vec = typename Vec<T>::type;
-  __shared__ vec sA[2][BN * 4];
-  __shared__ vec sB[2][BM * 4];
+  using opv = typename Op<T, Q8>::lds;
+  __shared__ opv sA[2][BN * 4];
+  __shared__ opv sB[2][BM * 4];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -46,14 +51,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   const int n0 = blockIdx.y * BN;
 
   // ---- per-thread staging coordinates (vector v = tid + it*256: row v>>2, k-vector v&3)
-  const T* arow[A_IT];
+  int64_t arow[A_IT];  // element offset of this thread's weight k-vector
   bool aval[A_IT];
 #pragma unroll
   for (int it = 0; it < A_IT; ++it) {
     const int v = tid + it * 256;
     const int co = n0 + (v >> 2);
     aval[it] = v < BN * 4 && co < p.Cout;
-    arow[it] = p.w + (int64_t)(aval[it] ? co : 0) * p.KPAD + (v & 3) * VEC;
+    arow[it] = (int64_t)(aval[it] ? co : 0) * p.KPAD + (v & 3) * VEC;
   }
   int bb[B_IT], biy[B_IT], bix[B_IT];
   int64_t bpix[B_IT];
@@ -72,7 +77,8 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
     biy[it] = oy * p.S - p.PAD;
     bix[it] = ox * p.S - p.PAD;
   }
-  vec ra[A_IT], rb[B_IT];
+  opv ra[A_IT];
+  vec rb[B_IT];
   // k-walk state: every staging vector of this thread has k-vector tid&3, so one (ky, kx, ci)
   // cursor serves all of them; it advances by BK per step with no integer division.
   int cur_ci = (tid & 3) * VEC, cur_kx = 0, cur_ky = 0;
@@ -94,7 +100,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   auto load_step = [&](int ks) {
     // every load is unconditional (clamped address) and masked afterwards: no branch per load
 #pragma unroll
-    for (int it = 0; it < A_IT; ++it) ra[it] = vload_sel(arow[it] + ks * BK, p.w, aval[it]);
+    for (int it = 0; it < A_IT; ++it) ra[it] = load_wop<T, Q8>(p.w, arow[it] + ks * BK, aval[it]);
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int v = tid + it * 256;
@@ -114,12 +120,12 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int v = tid + it * 256;
-      if (v < BN * 4) sA[buf][swz<0>(v >> 2, v & 3)] = ra[it];
+      if (v < BN * 4) sA[buf][swz<Q8>(v >> 2, v & 3)] = ra[it];
     }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int v = tid + it * 256;
-      if (v < BM * 4) sB[buf][swz<0>(v >> 2, v & 3)] = rb[it];
+      if (v < BM * 4) sB[buf][swz<Q8>(v >> 2, v & 3)] = to_op<T, Q8>(rb[it], p.qs);
     }
   };
 
@@ -136,15 +142,15 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   for (int ks = 0; ks < nsteps; ++ks) {
     const int buf = ks & 1;
     if (ks + 1 < nsteps) load_step(ks + 1);
-    vec af[TN], bf[TM];
+    opv af[TN], bf[TM];
 #pragma unroll
-    for (int i = 0; i < TN; ++i) af[i] = sA[buf][swz<0>(wn * TN * 16 + i * 16 + r16, g)];
+    for (int i = 0; i < TN; ++i) af[i] = sA[buf][swz<Q8>(wn * TN * 16 + i * 16 + r16, g)];
 #pragma unroll
-    for (int j = 0; j < TM; ++j) bf[j] = sB[buf][swz<0>(wm * TM * 16 + j * 16 + r16, g)];
+    for (int j = 0; j < TM; ++j) bf[j] = sB[buf][swz<Q8>(wm * TM * 16 + j * 16 + r16, g)];
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
     if (ks + 1 < nsteps) store_step(buf ^ 1);
     __syncthreads();
   }
@@ -160,7 +166,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   }
 #pragma unroll
   for (int i = 0; i < TN; ++i) co[i] = n0 + wn * TN * 16 + i * 16 + 4 * g;
-  conv_epilogue<T, TN, TM>(p, acc, pp, pv, co);
+  conv_epilogue<T, TN, TM, Q8>(p, acc, pp, pv, co);
 }
 
 // Spatial-tile 3x3 conv for thin inputs (Cin <= 32, the high-resolution backbone layers).
@@ -325,7 +331,7 @@ static bool try_tile(const ConvArgs<T>& a, int kh, hipStream_t s) {
 // tiles are summed through LDS in fixed wave order before the fused epilogue.
 // LDS rows are 16 vectors (4*BK elements), slot-swizzled with (kv ^ row) so both the staging
 // stores and the 16x16 fragment reads are bank-conflict-free.
-template <typename T, int BM, int BN, bool POINTWISE>
+template <typename T, int BM, int BN, bool POINTWISE, bool Q8>
 __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;    // per wave
@@ -334,11 +340,12 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   constexpr int A_IT = BN * 16 / 256, B_IT = BM * 16 / 256;
   static_assert(A_IT >= 1 && B_IT >= 1, "tile");
   using vec = typename Vec<T>::type;
-  constexpr int STAGE = 2 * (BN + BM) * 16;          // vectors, double-buffered
-  constexpr int RED = 4 * TN * TM * 64;              // f32x4 partials (16 B each = one vec)
-  __shared__ vec smem[STAGE > RED ? STAGE : RED];
-  vec* sA = smem;                                     // [2][BN*16]
-  vec* sB = smem + 2 * BN * 16;                       // [2][BM*16]
+  using opv = typename Op<T, Q8>::lds;
+  constexpr int STAGE = 2 * (BN + BM) * 16 * (int)sizeof(opv);  // bytes, double-buffered operands
+  constexpr int RED = 4 * TN * TM * 64 * 16;                      // bytes of f32x4 partials
+  __shared__ f32x4 smem[(STAGE > RED ? STAGE : RED) / 16];
+  opv* sA = reinterpret_cast<opv*>(smem);                         // [2][BN*16]
+  opv* sB = sA + 2 * BN * 16;                                     // [2][BM*16]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -346,13 +353,13 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const int kv = tid & 15;  // every staging vector of this thread has k-vector kv
 
-  const T* arow[A_IT];
+  int64_t arow[A_IT];  // element offset of this thread's weight k-vector
   bool aval[A_IT];
 #pragma unroll
   for (int it = 0; it < A_IT; ++it) {
     const int co = n0 + ((tid + it * 256) >> 4);
     aval[it] = co < p.Cout;
-    arow[it] = p.w + (int64_t)(aval[it] ? co : 0) * p.KPAD + kv * VEC;
+    arow[it] = (int64_t)(aval[it] ? co : 0) * p.KPAD + kv * VEC;
   }
   int bb[B_IT], biy[B_IT], bix[B_IT];
   int64_t bpix[B_IT];
@@ -376,12 +383,13 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     cur_ky = tap / p.KW;
     cur_kx = tap - cur_ky * p.KW;
   }
-  vec ra[A_IT], rb[B_IT];
+  opv ra[A_IT];
+  vec rb[B_IT];
   auto load_step = [&](int kb) {
     const int k = kb * BKB + kv * VEC;
     const bool kin = k < p.K;
 #pragma unroll
-    for (int it = 0; it < A_IT; ++it) ra[it] = vload_sel(arow[it] + kb * BKB, p.w, aval[it] && kin);
+    for (int it = 0; it < A_IT; ++it) ra[it] = load_wop<T, Q8>(p.w, arow[it] + kb * BKB, aval[it] && kin);
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       if constexpr (POINTWISE) {
@@ -409,7 +417,7 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int row = (tid + it * 256) >> 4;
-      sB[buf * BM * 16 + row * 16 + (kv ^ (row & 15))] = rb[it];
+      sB[buf * BM * 16 + row * 16 + (kv ^ (row & 15))] = to_op<T, Q8>(rb[it], p.qs);
     }
   };
 
@@ -427,7 +435,7 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   for (int kb = 0; kb < nsteps; ++kb) {
     const int buf = kb & 1;
     if (kb + 1 < nsteps) load_step(kb + 1);
-    vec af[TN], bf[TM];
+    opv af[TN], bf[TM];
 #pragma unroll
     for (int i = 0; i < TN; ++i) {
       const int row = i * 16 + r16;
@@ -441,7 +449,7 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
     if (kb + 1 < nsteps) store_step(buf ^ 1);
     __syncthreads();
   }
@@ -465,75 +473,85 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     const int64_t pp[1] = {m0 + j * 16 + r16};
     const bool pv[1] = {pp[0] < p.P};
     const int co[1] = {n0 + i * 16 + 4 * g};
-    conv_epilogue<T, 1, 1>(p, one, pp, pv, co);
+    conv_epilogue<T, 1, 1, Q8>(p, one, pp, pv, co);
   }
 }
 
-template <typename T, int BM, int BN>
+template <typename T, bool Q8, int BM, int BN>
 static void launch_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
   if (pointwise)
-    conv_wsk_kernel<T, BM, BN, true><<<grid, 256, 0, s>>>(a);
+    conv_wsk_kernel<T, BM, BN, true, Q8><<<grid, 256, 0, s>>>(a);
   else
-    conv_wsk_kernel<T, BM, BN, false><<<grid, 256, 0, s>>>(a);
+    conv_wsk_kernel<T, BM, BN, false, Q8><<<grid, 256, 0, s>>>(a);
 }
 
 // Wave-split-K where the block-tiled GEMM runs out of parallelism or k-depth per barrier:
 // K >= 1024, or K >= 512 on small maps (measured on DBL-n: 384->64 3x3 @40^2 112 -> 82 us,
 // 256->64 3x3 @20^2 47 -> 27 us; 64->64 3x3 @80^2 stays on conv_igemm_kernel, 47 vs 74 us).
-template <typename T>
+template <typename T, bool Q8>
 static bool try_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   if (!(a.K >= 1024 || (a.K >= 512 && a.P <= 16384))) return false;
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   const int64_t want = 768;
   if (a.Cout <= 32) {
-    if (blocks(128, 32) >= want) { launch_wsk<T, 128, 32>(a, pointwise, s); return true; }
-    launch_wsk<T, 64, 32>(a, pointwise, s);
+    if (blocks(128, 32) >= want) { launch_wsk<T, Q8, 128, 32>(a, pointwise, s); return true; }
+    launch_wsk<T, Q8, 64, 32>(a, pointwise, s);
     return true;
   }
   if (a.Cout <= 64) {
-    if (blocks(64, 64) >= want) { launch_wsk<T, 64, 64>(a, pointwise, s); return true; }
-    launch_wsk<T, 32, 64>(a, pointwise, s);
+    if (blocks(64, 64) >= want) { launch_wsk<T, Q8, 64, 64>(a, pointwise, s); return true; }
+    launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
     return true;
   }
-  if (blocks(32, 128) >= want || a.Cout % 128 == 0) { launch_wsk<T, 32, 128>(a, pointwise, s); return true; }
-  launch_wsk<T, 32, 64>(a, pointwise, s);
+  if (blocks(32, 128) >= want || a.Cout % 128 == 0) { launch_wsk<T, Q8, 32, 128>(a, pointwise, s); return true; }
+  launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
   return true;
 }
 
-template <typename T, int BM, int BN, int WM, int WN>
+template <typename T, bool Q8, int BM, int BN, int WM, int WN>
 static void launch_igemm(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
   if (pointwise)
-    conv_igemm_kernel<T, BM, BN, WM, WN, true><<<grid, 256, 0, s>>>(a);
+    conv_igemm_kernel<T, BM, BN, WM, WN, true, Q8><<<grid, 256, 0, s>>>(a);
   else
-    conv_igemm_kernel<T, BM, BN, WM, WN, false><<<grid, 256, 0, s>>>(a);
+    conv_igemm_kernel<T, BM, BN, WM, WN, false, Q8><<<grid, 256, 0, s>>>(a);
 }
 
-template <typename T>
+template <typename T, bool Q8>
 static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // BN covers Cout in one column of workgroups where it can (the input tile is then read once);
   // BM is the largest pixel tile that still gives >= 1024 workgroups (4 per CU) to fill the chip.
   const int64_t want = 1024;
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   if (a.Cout <= 16) {
-    if (blocks(256, 16) >= want) return launch_igemm<T, 256, 16, 4, 1>(a, pointwise, s);
-    if (blocks(128, 16) >= want) return launch_igemm<T, 128, 16, 4, 1>(a, pointwise, s);
-    return launch_igemm<T, 64, 16, 4, 1>(a, pointwise, s);
+    if (blocks(256, 16) >= want) return launch_igemm<T, Q8, 256, 16, 4, 1>(a, pointwise, s);
+    if (blocks(128, 16) >= want) return launch_igemm<T, Q8, 128, 16, 4, 1>(a, pointwise, s);
+    return launch_igemm<T, Q8, 64, 16, 4, 1>(a, pointwise, s);
   }
   if (a.Cout <= 32) {
-    if (blocks(256, 32) >= want) return launch_igemm<T, 256, 32, 4, 1>(a, pointwise, s);
-    if (blocks(128, 32) >= want) return launch_igemm<T, 128, 32, 4, 1>(a, pointwise, s);
-    return launch_igemm<T, 64, 32, 4, 1>(a, pointwise, s);
+    if (blocks(256, 32) >= want) return launch_igemm<T, Q8, 256, 32, 4, 1>(a, pointwise, s);
+    if (blocks(128, 32) >= want) return launch_igemm<T, Q8, 128, 32, 4, 1>(a, pointwise, s);
+    return launch_igemm<T, Q8, 64, 32, 4, 1>(a, pointwise, s);
   }
   if (a.Cout <= 64) {
-    if (blocks(128, 64) >= want) return launch_igemm<T, 128, 64, 2, 2>(a, pointwise, s);
-    if (blocks(64, 64) >= want) return launch_igemm<T, 64, 64, 2, 2>(a, pointwise, s);
-    return launch_igemm<T, 32, 64, 2, 2>(a, pointwise, s);
+    if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
+    if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
+    return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
   }
-  if (blocks(128, 128) >= want) return launch_igemm<T, 128, 128, 2, 2>(a, pointwise, s);
-  if (blocks(64, 128) >= want) return launch_igemm<T, 64, 128, 2, 2>(a, pointwise, s);
-  return launch_igemm<T, 32, 128, 2, 2>(a, pointwise, s);
+  if (blocks(128, 128) >= want) return launch_igemm<T, Q8, 128, 128, 2, 2>(a, pointwise, s);
+  if (blocks(64, 128) >= want) return launch_igemm<T, Q8, 64, 128, 2, 2>(a, pointwise, s);
+  return launch_igemm<T, Q8, 32, 128, 2, 2>(a, pointwise, s);
+}
+
+// Kernel choice: thin-input spatial tile (f16/f32 only), halo tile, wave-split-K, block GEMM.
+template <typename T, bool Q8>
+static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
+  static const bool no_halo = getenv("YDBL_NO_HALO") != nullptr;  // A/B switch for scripts/conv_bench.py
+  if (!Q8 && try_tile<T>(a, kh, s)) return;
+  if (!no_halo && try_conv3x3_halo<T, Q8>(a, kh, s)) return;
+  if (try_wsk<T, Q8>(a, pw, s)) return;
+  dispatch_conv<T, Q8>(a, pw, s);
 }
 
 template <typename T>
@@ -552,10 +570,15 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   a.y2 = reinterpret_cast<T*>(d->y2.ptr); a.y2cs = d->y2.cs;
   a.r2 = reinterpret_cast<const T*>(d->r2.ptr); a.r2cs = d->r2.cs;
   a.a2 = d->a2; a.b2 = d->b2;
+  a.dq = d->dq; a.qs = d->qscale;
   const bool pw = d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->x.h == d->y.h && d->x.w == d->y.w;
-  static const bool no_halo = getenv("YDBL_NO_HALO") != nullptr;  // A/B switch for scripts/conv_bench.py
-  if (!try_tile<T>(a, d->kh, s) && (no_halo || !try_conv3x3_halo<T>(a, d->kh, s)) && !try_wsk<T>(a, pw, s))
-    dispatch_conv<T>(a, pw, s);
+  if constexpr (sizeof(T) == 2) {
+    if (d->dq) {
+      route<T, true>(a, d->kh, pw, s);
+      return check_launch("ydbl_conv2d_nhwc");
+    }
+  }
+  route<T, false>(a, d->kh, pw, s);
   return check_launch("ydbl_conv2d_nhwc");
 }
 
@@ -584,6 +607,7 @@ extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
     if (d->r.n != d->y.n || d->r.h != d->y.h || d->r.w != d->y.w || d->r.c < d->y.c)
       return fail(YDBL_EINVAL, "conv: residual shape mismatch");
   }
+  if (d->dq && d->x.dtype != YDBL_F16) return fail(YDBL_EINVAL, "conv: fp8 operands need f16 activations");
   if (d->y2.ptr) {
     if (check_view(&d->y2, "conv.y2", false) || check_view(&d->r2, "conv.r2", false)) return YDBL_EINVAL;
     auto same = [&](const ydbl_view& v) {

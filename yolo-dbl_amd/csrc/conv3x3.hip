@@ -25,7 +25,7 @@ __device__ __forceinline__ int hslot(int pix, int g) {
   return (pix / (16 * S)) * (64 * S) + g * (16 * S) + (pix % S) * 16 + ((pix / S) & 15);
 }
 
-template <typename T, int S, int TH, int NTN>
+template <typename T, int S, int TH, int NTN, bool Q8>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int tiles_x, int tiles_y,
                                                               int co_splits) {
   constexpr int TW = 16;
@@ -38,8 +38,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   constexpr int XIT = (XSLOTS + 255) / 256, WIT = (WV + 255) / 256;
   constexpr int TMW = (TH + 3) / 4;  // 16-pixel tiles (= output rows) per wave
   using vec = typename Vec<T>::type;
-  __shared__ vec s_x[XSLOTS];
-  __shared__ vec s_w[WV];
+  using opv = typename Op<T, Q8>::lds;  // 8-byte e4m3 groups in fp8 mode (same slot layout)
+  __shared__ opv s_x[XSLOTS];
+  __shared__ opv s_w[WV];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     xok[it] = px < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
     xsrc[it] = p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + gv * VEC;
   }
-  const T* wsrc[WIT];
+  int64_t wsrc[WIT];  // element offsets into the weight matrix
   bool wok[WIT];
 #pragma unroll
   for (int it = 0; it < WIT; ++it) {  // slot = ((cb*9 + tap)*4 + g)*16 + r  ->  row cb*16 + r
@@ -81,19 +82,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     const int tap = t2 % 9, cb = t2 / 9;
     const int co = co0 + cb * 16 + r;
     wok[it] = co < p.Cout;
-    wsrc[it] = p.w + (int64_t)co * p.KPAD + tap * p.Cin + gv * VEC;
+    wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
-  vec xr[XIT], wr[WIT];
+  vec xr[XIT];
+  opv wr[WIT];
   auto load_chunk = [&](int c0) {
 #pragma unroll
     for (int it = 0; it < XIT; ++it) xr[it] = vload_sel(xsrc[it] + c0, p.x, xok[it]);
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) wr[it] = vload_sel(wsrc[it] + c0, p.w, wok[it]);
+    for (int it = 0; it < WIT; ++it) wr[it] = load_wop<T, Q8>(p.w, wsrc[it] + c0, wok[it]);
   };
   auto store_chunk = [&]() {
 #pragma unroll
     for (int it = 0; it < XIT; ++it)
-      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = xr[it];
+      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(xr[it], p.qs);
 #pragma unroll
     for (int it = 0; it < WIT; ++it)
       if (it * 256 + tid < WV) s_w[it * 256 + tid] = wr[it];
@@ -115,7 +117,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap % 3;
-      vec af[NTN], bf[TMW];
+      opv af[NTN], bf[TMW];
 #pragma unroll
       for (int i = 0; i < NTN; ++i) af[i] = s_w[((i * 9 + tap) * 4 + g) * 16 + r16];
 #pragma unroll
@@ -126,7 +128,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
 #pragma unroll
       for (int j = 0; j < TMW; ++j)
 #pragma unroll
-        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_chunk<T>(af[i], bf[j], acc[i][j]);
+        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
     }
     if (ch + 1 < nchunks) {
       __syncthreads();  // every wave is done reading this chunk
@@ -147,18 +149,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   int co[NTN];
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
-  conv_epilogue<T, NTN, TMW>(p, acc, pp, pv, co);
+  conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co);
 }
 
-template <typename T, int S, int TH>
+template <typename T, bool Q8, int S, int TH>
 static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   if (a.Cout <= 32) {
-    conv3x3_halo_kernel<T, S, TH, 2><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else {
     const int cs = (int)cdiv(a.Cout, 64);
-    conv3x3_halo_kernel<T, S, TH, 4><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 4, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   }
 }
 
@@ -170,7 +172,7 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
 // 714 -> 382 us, 768->128 @40^2 bs64 534 -> 348 us, 1024->128 @160^2 bs8 1371 -> 688 us.
 // 16-row tiles where the map allows (weights staged once per 256 pixels instead of 128),
 // 4-row tiles when 8-row tiles would leave fewer than 512 workgroups.
-template <typename T>
+template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   constexpr int BK = 4 * Vec<T>::N;
   if (kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
@@ -180,13 +182,14 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   const int64_t csplit = cdiv(a.Cout, 64);
   const int64_t tiles8 = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * csplit;
   const int64_t tiles16 = (int64_t)a.N * cdiv(a.Ho, 16) * cdiv(a.Wo, 16) * csplit;
-  if (a.Ho % 16 == 0 && a.Cout > 32 && tiles16 >= 512) launch_halo<T, 1, 16>(a, s);
-  else if (tiles8 < 512) launch_halo<T, 1, 4>(a, s);
-  else launch_halo<T, 1, 8>(a, s);
+  if (a.Ho % 16 == 0 && a.Cout > 32 && tiles16 >= 512) launch_halo<T, Q8, 1, 16>(a, s);
+  else if (tiles8 < 512) launch_halo<T, Q8, 1, 4>(a, s);
+  else launch_halo<T, Q8, 1, 8>(a, s);
   return true;
 }
 
-template bool try_conv3x3_halo<_Float16>(const ConvArgs<_Float16>&, int, hipStream_t);
-template bool try_conv3x3_halo<float>(const ConvArgs<float>&, int, hipStream_t);
+template bool try_conv3x3_halo<_Float16, false>(const ConvArgs<_Float16>&, int, hipStream_t);
+template bool try_conv3x3_halo<_Float16, true>(const ConvArgs<_Float16>&, int, hipStream_t);
+template bool try_conv3x3_halo<float, false>(const ConvArgs<float>&, int, hipStream_t);
 
 }  // namespace ydbl

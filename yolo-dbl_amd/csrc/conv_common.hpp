@@ -17,10 +17,55 @@ struct ConvArgs {
   T* y2; int y2cs;  // optional second output y2 = a2 * T(v) + b2 * r2 (fused FullPAD)
   const T* r2; int r2cs;
   float a2, b2;
+  // fp8 operand mode (dq != nullptr): w holds OCP e4m3 bytes [Cout][KPAD] (per-output-channel
+  // scale sw), activations are quantized to e4m3 with the per-tensor scale qs as they are staged,
+  // and the accumulator is dequantized by dq[co] = 1 / (sw[co] * qs) before bias / activation.
+  const float* dq;
+  float qs;
 };
 
+// ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------
+template <typename T, bool Q8> struct Op {
+  using lds = typename Vec<T>::type;
+};
+template <> struct Op<_Float16, true> {
+  using lds = uint64_t;
+};
+
+// 8 activations -> 8 OCP e4m3 bytes (k order kept: byte i = element i), scaled and saturated
+__device__ __forceinline__ uint64_t quant_e4m3(const h8& v, float s) {
+  float f[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = fminf(fmaxf(float(v[i]) * s, -448.f), 448.f);
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[4], f[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(f[6], f[7], hi, true);
+  return (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32);
+}
+
+template <typename T, bool Q8>
+__device__ __forceinline__ typename Op<T, Q8>::lds to_op(const typename Vec<T>::type& v, float s) {
+  if constexpr (Q8) return quant_e4m3(v, s);
+  else return v;
+}
+
+// weight (A operand) load of one k-vector: VEC elements of T, or 8 e4m3 bytes at the same
+// element offset (the fp8 matrix is [Cout][KPAD] bytes)
+template <typename T, bool Q8>
+__device__ __forceinline__ typename Op<T, Q8>::lds load_wop(const T* w, int64_t off, bool ok) {
+  if constexpr (Q8) {
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(w);
+    const uint64_t v = *reinterpret_cast<const uint64_t*>(b + (ok ? off : 0));
+    return ok ? v : 0ull;
+  } else {
+    return vload_sel(w + off, w, ok);
+  }
+}
+
+
 // conv3x3.hip: halo-tiled 3x3 kernel for Cin >= 2 k-steps; false when the shape is not its own.
-template <typename T>
+template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s);
 
 template <typename T>
@@ -39,10 +84,17 @@ __device__ __forceinline__ f32x4 mfma_chunk<float>(const f32x4& a, const f32x4& 
   return c;
 }
 
+// one MFMA k-step on policy operands (fp8: v_mfma_f32_16x16x32_fp8_fp8, 8 e4m3 per lane)
+template <typename T, bool Q8>
+__device__ __forceinline__ f32x4 mfma_op(const typename Op<T, Q8>::lds& a, const typename Op<T, Q8>::lds& b, f32x4 c) {
+  if constexpr (Q8) return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8((long)a, (long)b, c, 0, 0, 0);
+  else return mfma_chunk<T>(a, b, c);
+}
+
 // Epilogue of one wave's TN x TM accumulator tiles: lane owns output channels co[i]..co[i]+3 of
 // pixel pp[j].  Every load is unconditional from a clamped address (bias once; the residual of a
 // pixel for all TN tiles at once) so the loads overlap; only the stores are predicated.
-template <typename T, int TN, int TM>
+template <typename T, int TN, int TM, bool Q8 = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 (&acc)[TN][TM],
                                               const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN]) {
   const bool c4 = (p.Cout & 3) == 0;  // uniform: co..co+3 in range whenever co < Cout
@@ -61,6 +113,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
       for (int q = 0; q < 4; ++q) bv[i][q] = 0.f;
     }
   }
+  float dqv[TN][4];  // fp8 dequant factors (constant 1 folds away in the f16/f32 paths)
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dqv[i][q] = Q8 ? p.dq[min(co[i] + q, p.Cout - 1)] : 1.f;
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     const int64_t pc = pv[j] ? pp[j] : 0;
@@ -81,7 +138,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
     for (int i = 0; i < TN; ++i) {
       float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[i][j][q] + bv[i][q], p.act);
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[i][j][q] * dqv[i][q] + bv[i][q], p.act);
       if (p.res == YDBL_RES_ADD) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = rv[i][q] + v[q];

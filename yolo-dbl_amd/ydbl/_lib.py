@@ -30,7 +30,8 @@ class ConvDesc(C.Structure):
     _fields_ = [("x", View), ("y", View), ("r", View), ("w", C.c_void_p), ("bias", C.c_void_p),
                 ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32), ("dil", C.c_int32),
                 ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32),
-                ("y2", View), ("r2", View), ("a2", C.c_float), ("b2", C.c_float)]
+                ("y2", View), ("r2", View), ("a2", C.c_float), ("b2", C.c_float),
+                ("dq", C.c_void_p), ("qscale", C.c_float)]
 
 
 class DwConvDesc(C.Structure):

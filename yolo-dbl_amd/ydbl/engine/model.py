@@ -21,7 +21,7 @@ from ..nn.tasks import DetectionModel
 from .results import Results
 from .session import DetectSession
 
-DEFAULTS = {"conf": 0.25, "iou": 0.7, "max_det": 300, "half": False, "device": None, "agnostic_nms": False,
+DEFAULTS = {"conf": 0.25, "iou": 0.7, "max_det": 300, "half": False, "fp8": False, "device": None, "agnostic_nms": False,
             "classes": None, "batch": 1, "verbose": False}
 
 
@@ -123,16 +123,17 @@ class Model:
 
     # ------------------------------------------------------------------ inference
     def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
-                multi_label=False, device=None, keep_pred=False, use_graph=True) -> DetectSession:
+                multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False) -> DetectSession:
         dev = select_device(device)
-        dtype = torch.float16 if half else torch.float32
+        dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
-               tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph)
+               tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
+               bool(fp8))
         s = self._sessions.get(key)
         if s is None:
             with torch.cuda.device(dev):
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
-                                  keep_pred=keep_pred, use_graph=use_graph, device=dev)
+                                  keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8)
             self._sessions[key] = s
         return s
 
@@ -145,7 +146,7 @@ class Model:
         im = im.to(dev, non_blocking=True).float()
         b, _, h, w = im.shape
         s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
-                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev)
+                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"])
         t1 = time.perf_counter()
         det, cnt = s(im)
         counts = cnt.tolist()  # one sync per batch

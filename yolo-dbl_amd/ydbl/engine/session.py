@@ -21,8 +21,11 @@ from ..runtime import GraphRunner, Plan
 class DetectSession:
     def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
                  multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
-                 keep_pred=False, use_graph=True, device="cuda"):
+                 keep_pred=False, use_graph=True, device="cuda", fp8=False):
+        if fp8 and dtype != torch.float16:
+            raise ValueError("fp8 operands run on the fp16 activation path (half=True)")
         self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
+        self.fp8, self.fp8_ready = bool(fp8), False
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         cm = model.compile(batch, h, w, dtype, device=device)
         self.compiled = cm
@@ -72,7 +75,21 @@ class DetectSession:
             raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
         self.compiled.input.copy_(x, non_blocking=True)
 
+    def calibrate_fp8(self, x: torch.Tensor | None = None) -> int:
+        """Switch the dense convs to e4m3 operands (ydbl.quant), with activation scales from one fp16
+        pass over `x` (default: the batch already loaded).  Returns the number of convs switched."""
+        from ..quant import enable_fp8
+
+        if x is not None:
+            self.load(x)
+        n = enable_fp8(self.plan, self.plan.run)
+        self._graph = None  # descriptors changed: recapture
+        self.fp8_ready = True
+        return n
+
     def launch(self):
+        if self.fp8 and not self.fp8_ready:
+            self.calibrate_fp8()  # first batch calibrates (dynamic post-training quantization)
         if self.use_graph:
             if self._graph is None:
                 self._graph = GraphRunner(self.plan)

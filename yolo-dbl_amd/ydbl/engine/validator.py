@@ -38,7 +38,7 @@ class DetectionValidator:
             s = self.model.session(b, h, w, half=self.args.get("half", False), conf=self.args["conf"],
                                    iou=self.args["iou"], max_det=self.args.get("max_det", 300), multi_label=True,
                                    agnostic=self.args.get("agnostic_nms", False) or self.args.get("single_cls", False),
-                                   device=dev)
+                                   device=dev, fp8=self.args.get("fp8", False))
             det, cnt = s(im)
             det, cnt = det.cpu(), cnt.cpu().tolist()
             bidx = torch.as_tensor(batch["batch_idx"]).cpu()

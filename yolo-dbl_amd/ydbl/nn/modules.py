@@ -77,14 +77,16 @@ def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None
         wt = torch.nn.functional.pad(wt, (0, x.c - ci))
     K = kh * kw * x.c
     kpad = round_up(K, 32)
-    wk = torch.nn.functional.pad(wt.reshape(co, K), (0, kpad - K)).to(plan.dtype)
-    wd = plan.const(wk)
+    wk32 = torch.nn.functional.pad(wt.reshape(co, K).float(), (0, kpad - K))
+    wd = plan.const(wk32.to(plan.dtype))
     bd = plan.const(b.float()) if b is not None else None
     d = ConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(), wd.data_ptr(),
                  bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, kpad, act, res_mode,
-                 _null_view(), _null_view(), 0.0, 0.0)
+                 _null_view(), _null_view(), 0.0, 0.0, None, 1.0)
     plan.launch("ydbl_conv2d_nhwc", d, what=what, keep=[wd, bd, d])
     plan.note_writer(y, d)
+    if plan.dtype == torch.float16 and x.c >= 64 and not what.startswith("Detect."):
+        plan.fp8_candidates.append((d, x, wk32))  # see ydbl.quant: e4m3 operands after calibration
 
 
 def emit_dw(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,

@@ -1,0 +1,54 @@
+"""fp8 (OCP e4m3) operands for the dense convolutions: BASELINE config 5 ("fp8 weights+activations on
+CDNA4 fp8 MFMA, mAP drop reported").
+
+Post-training, calibration-based, per layer:
+  - weights: per-output-channel scale sw = 448 / max|w[co]|, w_q = e4m3(w * sw) stored as bytes;
+  - activations: per-tensor scale qs = 448 / max|x| of the layer's input over a calibration batch,
+    x_q = e4m3(sat(x * qs)) applied by the conv kernels while staging into LDS;
+  - the kernels run v_mfma_f32_16x16x32_fp8_fp8 and dequantize the fp32 accumulator with
+    dq[co] = 1 / (sw[co] * qs) before bias + activation (include/ydbl.h, ydbl_conv_desc).
+Layers kept in fp16: convs with fewer than 64 input channels (stem and the thin high-resolution
+backbone convs), depthwise / DSConv / attention / hypergraph kernels, and the Detect head's
+final box / class 1x1 convs.  Activations are stored in fp16 between layers.
+"""
+
+from __future__ import annotations
+
+import torch
+
+E4M3_MAX = 448.0
+
+
+def quantize_weights_e4m3(w: torch.Tensor):
+    """[Cout][K] fp32 -> (e4m3 bytes [Cout][K] uint8, per-row scale sw [Cout] fp32)."""
+    amax = w.abs().amax(dim=1).clamp_min(1e-12)
+    sw = E4M3_MAX / amax
+    q = (w * sw[:, None]).clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), sw
+
+
+def enable_fp8(plan, run_calibration, select=None) -> int:
+    """Calibrate activation scales with one fp16 pass and switch every fp8 candidate conv of `plan`
+    to e4m3 operands.  `run_calibration()` must execute the plan once on calibration images.
+    Returns the number of convolutions switched."""
+    run_calibration()
+    torch.cuda.synchronize(plan.device)
+    cands = [c for i, c in enumerate(plan.fp8_candidates) if select is None or select(i)]
+    if not cands:
+        return 0
+    amaxes = torch.stack([x.torch().abs().amax().float() for _, x, _ in cands]).cpu()
+    for (d, _x, w32), ax in zip(cands, amaxes.tolist()):
+        qs = E4M3_MAX / ax if ax > 0 else 1.0
+        wq, sw = quantize_weights_e4m3(w32)
+        wd = plan.const(wq.contiguous())
+        dq = plan.const((1.0 / (sw * qs)).float())
+        d.w = wd.data_ptr()
+        d.dq = dq.data_ptr()
+        d.qscale = float(qs)
+    plan.fp8_enabled = True
+    return len(cands)
+
+
+def e4m3_round(t: torch.Tensor) -> torch.Tensor:
+    """Round-trip through OCP e4m3 (saturating), fp32 result: the CPU emulation used by the tests."""
+    return t.clamp(-E4M3_MAX, E4M3_MAX).to(torch.float8_e4m3fn).float()

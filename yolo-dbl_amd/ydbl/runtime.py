@@ -85,6 +85,7 @@ class Plan:
         self.buffers: list[torch.Tensor] = []
         self.bytes_allocated = 0
         self._writers: dict = {}  # view key -> (step index, ConvDesc) of the dense conv that wrote it
+        self.fp8_candidates: list = []  # (ConvDesc, input view, fp32 [Cout][KPAD] weights) of fp8-able convs
 
     # ---------------------------------------------------------------- memory
     def alloc(self, n: int, h: int, w: int, c: int, dtype: torch.dtype | None = None, cs: int | None = None) -> TV:
