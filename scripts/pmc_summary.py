@@ -14,9 +14,9 @@ import sys
 from collections import defaultdict
 
 FAMILIES = {  # name keys, FETCH_SIZE multiplier
-    "conv2d": (("conv_igemm_kernel", "conv3x3_tile_kernel", "conv_wsk_kernel"), 2),
+    "conv2d": (("conv_igemm_kernel", "conv3x3_tile_kernel", "conv_wsk_kernel", "conv3x3_halo_kernel"), 2),
     "dsconv": (("dsconv_kernel",), 2),
-    "stem": (("stem_kernel",), 1),
+    "stem": (("stem_kernel",), 2),
     "dwconv": (("dwconv_lds_kernel", "dwconv_kernel"), 2),
     "nms": (("nms_kernel",), 1),
 }
