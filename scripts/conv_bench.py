@@ -22,6 +22,7 @@ SHAPES = [  # (cin, cout, k, s, H[, B])
     (512, 64, 3, 1, 80, 64), (768, 128, 3, 1, 40, 64), (384, 128, 3, 1, 40, 64), (128, 128, 3, 1, 80, 64),
     (1024, 128, 3, 1, 160, 8), (128, 256, 3, 2, 320, 8), (64, 128, 3, 1, 320, 8), (1024, 256, 1, 1, 40, 64),
     (1280, 256, 1, 1, 160, 8), (2048, 512, 1, 1, 80, 8),
+    (128, 192, 1, 1, 40), (320, 128, 1, 1, 40), (256, 128, 1, 1, 20), (128, 128, 1, 1, 20),  # 32..35
 ]
 
 

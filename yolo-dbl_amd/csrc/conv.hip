@@ -521,8 +521,12 @@ static void launch_igemm(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
 template <typename T, bool Q8>
 static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // BN covers Cout in one column of workgroups where it can (the input tile is then read once);
-  // BM is the largest pixel tile that still gives >= 1024 workgroups (4 per CU) to fill the chip.
-  const int64_t want = 1024;
+  // BM is the largest pixel tile that still gives >= `want` workgroups: 512 (2 per CU) for small
+  // maps whose Cout fits one 128-wide column (bigger pixel tiles re-read the weights less:
+  // 512->128 1x1 @40^2 bs32 31.3 -> 23.0 us, 384->128 25.6 -> 19.4 us), 1024 otherwise
+  // (128->192: 16.4 vs 21.4 us; DBL-s bs64 end to end 0.8 % faster at 1024).
+  static const char* ov = getenv("YDBL_IGEMM_WANT");  // A/B knob for the benches
+  const int64_t want = ov && *ov ? atoi(ov) : (a.Cout <= 128 && a.P <= 65536 ? 512 : 1024);
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   if (a.Cout <= 16) {
     if (blocks(256, 16) >= want) return launch_igemm<T, Q8, 256, 16, 4, 1>(a, pointwise, s);
