@@ -89,9 +89,11 @@ typedef struct {
 int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream);
 
 /* DSConv in one kernel (conv.py:91-108): y = act(pw(dw(x)) + bias) [+ r], BN folded into pw.
- * dw_w fp32 [k*k][cin] (no dw bias), pw_w [cout][kpad] in the view dtype (kpad = round_up(cin, 32),
- * zero padded), bias fp32 [cout].  cin multiple of 32 (f16) / 16 (f32).  The depthwise output is
- * rounded to the view dtype (the reference's intermediate tensor) and never leaves LDS. */
+ * dw_w fp32 [k*k][cin], pw_w [cout][kpad] in the view dtype (kpad = round_up(cin, 32), zero
+ * padded), bias fp32 [cout].  cin multiple of 32 (f16) / 16 (f32).  The depthwise output is
+ * rounded to the view dtype (the reference's intermediate tensor) and never leaves LDS.
+ * dw_bias (fp32 [cin] or NULL) and dw_act extend it to the Detect head's DWConv -> Conv1x1 pair
+ * (head.py:93-101: dw = SiLU(BN(dwconv)), folded): dw output = dw_act(dw(x) + dw_bias). */
 typedef struct {
   ydbl_view x, y, r;
   const float* dw_w;
@@ -99,6 +101,8 @@ typedef struct {
   const float* bias;
   int32_t k, stride, pad, dil;
   int32_t kpad, act, res_mode;
+  const float* dw_bias;
+  int32_t dw_act;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 

@@ -200,6 +200,37 @@ def test_conv_fp8(cin, cout, k, n, h, w, res):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("c,c2,shape", [(64, 64, (2, 64, 40, 40)), (128, 64, (2, 128, 20, 21)), (64, 80, (1, 64, 13, 17))])
+def test_detect_dw_pw_fused(dtype, c, c2, shape):
+    """Detect cv3 pair DWConv(c,c,3) -> Conv(c,c2,1) (head.py:93-101) as one fused depthwise->pointwise
+    launch: dw bias + SiLU applied in LDS before the pointwise MFMA."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(c + c2)
+    ref = torch.nn.Sequential(om.DWConv(c, c, 3), om.Conv(c, c2, 1)).eval()
+    with torch.no_grad():
+        for bn in [m for m in ref.modules() if isinstance(m, torch.nn.BatchNorm2d)]:
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 2.0)
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    dwc, pwc = M.DWConv(c, c, 3), M.Conv(c, c2, 1)
+    dwc.load_state_dict(ref[0].state_dict())
+    pwc.load_state_dict(ref[1].state_dict())
+    x = torch.randn(*shape)
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x)
+    y = M.emit_dw_pw(plan, dwc, pwc, xv)
+    assert [st.fn.__name__ for st in plan.steps] == ["ydbl_dsconv_nhwc"]
+    _run(plan)
+    with torch.no_grad():
+        r = ref(x.to(dtype).float())
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(y.nchw().float().cpu(), r, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("late", ["x0", "x1"])
 def test_fullpad_fused_into_conv(dtype, late):
     """FullPAD_Tunnel (block.py:1954-1956) on conv outputs becomes the producing conv's second output:

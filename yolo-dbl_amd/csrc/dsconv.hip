@@ -33,7 +33,8 @@ __device__ __forceinline__ void store4(float* d, const float* a) {
 }
 
 template <typename T, int K, int S, int DIL, int TH, int TW, int CSEG, int NTN, bool DBUF>
-__global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const float* __restrict__ dww, int tiles_x,
+__global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const float* __restrict__ dww,
+                                                        const float* __restrict__ dwb, int dw_act, int tiles_x,
                                                         int tiles_y, int co_splits) {
   constexpr int VEC = Vec<T>::N;
   constexpr int CC = 4 * VEC;    // channels per chunk (one pointwise MFMA k-step)
@@ -157,6 +158,13 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
 #pragma unroll
             for (int e = 0; e < 4; ++e) a[c][e] = fmaf(xs[c * S + kx * DIL][e], wv[kx][e], a[c][e]);
       }
+      if (dwb) {  // uniform: DWConv (+ folded BN) bias and activation before the pointwise
+        const f32x4 bq = *reinterpret_cast<const f32x4*>(dwb + c0 + q * 4);
+#pragma unroll
+        for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[c][e] = apply_act(a[c][e] + bq[e], dw_act);
+      }
 #pragma unroll
       for (int c = 0; c < CSEG; ++c) {
         const int px = r * TW + sg * CSEG + c;
@@ -202,12 +210,12 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
 }
 
 template <typename T, int K, int S, int DIL, int TH, int TW, int CSEG, bool DBUF = true>
-static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, hipStream_t s) {
+static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   auto go = [&](auto kern, int ntn) {
     const int cs = (int)cdiv(a.Cout, ntn * 16);
-    kern<<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, dww, tiles_x, tiles_y, cs);
+    kern<<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y, cs);
   };
   if (a.Cout <= 32) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
   else if (a.Cout <= 64 || ntiles < 256) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
@@ -219,9 +227,9 @@ static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, hipStream_t s
 // hide each other's halo loads; 40^2 k7 64ch 25.8 -> 15.1 us); 20-px and smaller maps take an 8x8
 // double-buffered tile (more workgroups on the few pixels).
 template <typename T, int K, int S, int DIL>
-static int launch_ds(const ConvArgs<T>& a, const float* dww, hipStream_t s) {
-  if (a.Wo > 20) launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, s);
-  else launch_ds_tile<T, K, S, DIL, 8, 8, 2, true>(a, dww, s);
+static int launch_ds(const ConvArgs<T>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
+  if (a.Wo > 20) launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, dwb, dw_act, s);
+  else launch_ds_tile<T, K, S, DIL, 8, 8, 2, true>(a, dww, dwb, dw_act, s);
   return check_launch("ydbl_dsconv_nhwc");
 }
 
@@ -238,10 +246,10 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
   a.K = d->x.c; a.KPAD = d->kpad;
   a.act = d->act; a.res = d->res_mode;
   a.P = d->y.n * d->y.h * d->y.w;
-  if (d->k == 3 && d->stride == 1 && d->dil == 1) return launch_ds<T, 3, 1, 1>(a, d->dw_w, s);
-  if (d->k == 3 && d->stride == 2 && d->dil == 1) return launch_ds<T, 3, 2, 1>(a, d->dw_w, s);
-  if (d->k == 5 && d->stride == 1 && d->dil == 1) return launch_ds<T, 5, 1, 1>(a, d->dw_w, s);
-  if (d->k == 7 && d->stride == 1 && d->dil == 1) return launch_ds<T, 7, 1, 1>(a, d->dw_w, s);
+  if (d->k == 3 && d->stride == 1 && d->dil == 1) return launch_ds<T, 3, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
+  if (d->k == 3 && d->stride == 2 && d->dil == 1) return launch_ds<T, 3, 2, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
+  if (d->k == 5 && d->stride == 1 && d->dil == 1) return launch_ds<T, 5, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
+  if (d->k == 7 && d->stride == 1 && d->dil == 1) return launch_ds<T, 7, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
   return fail(YDBL_EINVAL, "dsconv: supported (k, stride, dil): (3,1,1) (3,2,1) (5,1,1) (7,1,1)");
 }
 

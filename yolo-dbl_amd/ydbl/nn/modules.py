@@ -135,22 +135,40 @@ def fused_dsconv_ok(dw: nn.Conv2d, x: TV, dtype) -> bool:
 
 
 def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Tensor, b_pw: torch.Tensor,
-                act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv") -> TV:
-    """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA."""
+                act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv",
+                w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE) -> TV:
+    """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA.
+    w_dw / b_dw / dw_act: folded DWConv weights, bias and activation (Detect's DWConv -> Conv1x1 pair)."""
     k, st, p, d = dw.kernel_size[0], dw.stride[0], dw.padding[0], dw.dilation[0]
     c = x.c
     co = w_pw.shape[0]
     ho, wo = conv_out_hw(x.h, x.w, k, st, p, d)
     y = out if out is not None else plan.alloc(x.n, ho, wo, co)
     assert (y.h, y.w, y.c) == (ho, wo, co), ((y.h, y.w, y.c), (ho, wo, co))
-    dww = plan.const(dw.weight.detach().float().cpu().reshape(c, k * k).t().contiguous())
+    wdw = (dw.weight if w_dw is None else w_dw).detach().float().cpu()
+    dww = plan.const(wdw.reshape(c, k * k).t().contiguous())
     kpad = round_up(c, 32)
     pww = plan.const(torch.nn.functional.pad(w_pw.reshape(co, c).float(), (0, kpad - c)).to(plan.dtype))
     bd = plan.const(b_pw.float())
+    dwb = plan.const(b_dw.float()) if b_dw is not None else None
     desc = _lib.DsConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(),
-                           dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode)
-    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, desc])
+                           dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode,
+                           dwb.data_ptr() if dwb is not None else None, dw_act)
+    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, dwb, desc])
     return y
+
+
+def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = None, what="DWConv+Conv1x1") -> TV:
+    """nn.Sequential(DWConv(c, c, k), Conv(c, c2, 1)) of the Detect head (head.py:93-101): one fused launch
+    when the shapes allow (the depthwise output stays in LDS), else two."""
+    if fused_dsconv_ok(dwc.conv, x, plan.dtype) and pwc.conv.kernel_size == (1, 1) and pwc.conv.stride == (1, 1):
+        wd, bdw = dwc.folded()
+        wp, bp = pwc.folded()
+        if bdw is None:
+            bdw = torch.zeros(x.c)
+        return emit_dsconv(plan, dwc.conv, x, out, wp, bp if bp is not None else torch.zeros(wp.shape[0]),
+                           _act_code(pwc.act), what=what, w_dw=wd, b_dw=bdw, dw_act=_act_code(dwc.act))
+    return pwc.emit(plan, dwc.emit(plan, x), out)
 
 
 def stem_ok(m, ch: int) -> bool:
@@ -707,9 +725,9 @@ class Detect(nn.Module):
             if self.legacy:
                 u = self.cv3[i][0].emit(plan, x)
                 u = self.cv3[i][1].emit(plan, u)
-            else:
-                u = emit_seq(plan, self.cv3[i][0], x)
-                u = emit_seq(plan, self.cv3[i][1], u)
+            else:  # [DWConv, Conv1x1] x 2: each pair is one fused depthwise -> pointwise launch
+                u = emit_dw_pw(plan, self.cv3[i][0][0], self.cv3[i][0][1], x)
+                u = emit_dw_pw(plan, self.cv3[i][1][0], self.cv3[i][1][1], u)
             emit_conv2d(plan, self.cv3[i][2], u, lv.cslice(4 * self.reg_max, self.nc), what="Detect.cls")
             levels.append(lv)
         return levels
