@@ -24,6 +24,9 @@
  *   ydbl_dsconv_nhwc       <- DSConv.forward conv.py:91-108 (dw + pw + BN + SiLU, one kernel)
  *   ydbl_dwconv2d_nhwc     <- depthwise nn.Conv2d (DSConv.dw conv.py:98, DWConv conv.py:128-133,
  *                             GhostConv.cv2 conv.py:194, LSKblock.conv0/conv_spatial LSKA.py:31-32)
+ *   ydbl_letterbox         <- BasePredictor.preprocess engine/predictor.py:116-134 for ndarray frames:
+ *                             LetterBox.__call__ data/augment.py:1535-1597 (cv2.resize INTER_LINEAR,
+ *                             copyMakeBorder 114) + BGR->RGB + HWC->CHW + float /255
  *   ydbl_input_nchw_to_nhwc<- BasePredictor.preprocess engine/predictor.py:116-134 (+ LoadTensor /255)
  *   ydbl_conv_stem         <- preprocess (predictor.py:116-134) fused with the first backbone Conv
  *                             (conv.py:39-63 after fuse), reading the NCHW fp32 batch directly
@@ -39,6 +42,9 @@
  *   ydbl_nms               <- utils/ops.py:278-310 (+ torchvision.ops.nms, torchvision 0.23.0),
  *                             with clip_boxes utils/ops.py:319-338 as reached through
  *                             scale_boxes :92-127 for tensor sources (gain 1, pad 0)
+ *   ydbl_match_predictions <- DetectionValidator._process_batch models/yolo/detect/val.py:209-227
+ *                             (box_iou utils/metrics.py:52-71 + BaseValidator.match_predictions
+ *                             engine/validator.py:222-262, non-scipy branch)
  */
 #ifndef YDBL_H
 #define YDBL_H
@@ -225,6 +231,40 @@ typedef struct {
 } ydbl_nms_desc;
 int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms);
 int ydbl_nms(const ydbl_nms_desc* d, void* stream);
+
+/* LetterBox a batch of HWC uint8 BGR frames into one fp32 NCHW RGB canvas batch (values /255).
+ * src: frames back to back, frame i at src + src_off[i] (int64 device array);
+ * meta int32 device array [n][6] = (h, w, unpad_h, unpad_w, top, left) as LetterBox computes them
+ * on the host; out fp32 [n][3][out_h][out_w]; pad_value is the border colour (114).
+ * Resize = OpenCV 4.x uint8 INTER_LINEAR (see letterbox.hip for the exact fixed-point rules). */
+typedef struct {
+  const uint8_t* src; const int64_t* src_off; const int32_t* meta;
+  int32_t n, out_h, out_w;
+  float pad_value;
+  float* out;
+} ydbl_letterbox_desc;
+int ydbl_letterbox(const ydbl_letterbox_desc* d, void* stream);
+
+/* mAP true-positive matrix of a batch of NMS outputs against ground-truth labels.
+ * det fp32 [n][max_det][6] (x1,y1,x2,y2,conf,cls) + det_count int32 [n] (ydbl_nms outputs);
+ * labels grouped by image: gt_box fp32 [n_gt][4] xyxy, gt_cls fp32 [n_gt], gt_ofs int32 [n+1]
+ * (image b owns labels gt_ofs[b] .. gt_ofs[b+1]-1, gt_ofs[n] == n_gt, original order kept);
+ * iouv fp32 [n_iou] thresholds; single_cls: detections count as class 0.
+ * correct uint8 [n][max_det][n_iou]: 1 where the detection is a TP at that IoU threshold
+ * (rows >= det_count are zeroed).  Bit-exact with the reference for distinct IoUs; an exact IoU
+ * tie between two same-class labels of one detection resolves to the larger label index. */
+typedef struct {
+  const float* det; const int32_t* det_count;
+  int32_t n, max_det;
+  const float* gt_box; const float* gt_cls; const int32_t* gt_ofs;
+  int32_t n_gt;
+  const float* iouv; int32_t n_iou;
+  int32_t single_cls;
+  uint8_t* correct;
+  void* workspace; /* ydbl_match_workspace(n, max_det, n_gt, n_iou) bytes */
+} ydbl_match_desc;
+int64_t ydbl_match_workspace(int32_t n, int32_t max_det, int32_t n_gt, int32_t n_iou);
+int ydbl_match_predictions(const ydbl_match_desc* d, void* stream);
 
 const char* ydbl_last_error(void);
 const char* ydbl_version(void);

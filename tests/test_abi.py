@@ -40,6 +40,8 @@ STRUCTS = {
     "ydbl_decode_desc": "DecodeDesc",
     "ydbl_pred_cand_desc": "PredCandDesc",
     "ydbl_nms_desc": "NmsDesc",
+    "ydbl_match_desc": "MatchDesc",
+    "ydbl_letterbox_desc": "LetterboxDesc",
 }
 
 
@@ -80,6 +82,11 @@ def test_validation_errors_without_gpu():
     assert lib.ydbl_nms(nd, None) == 1
     with pytest.raises(_lib.YdblError):
         _lib.check(lib.ydbl_nms(nd, None), "ydbl_nms")
+    md = _lib.MatchDesc()
+    assert lib.ydbl_match_predictions(md, None) == 1
+    assert "null buffer" in lib.ydbl_last_error().decode()
+    assert lib.ydbl_letterbox(_lib.LetterboxDesc(), None) == 1
+    assert lib.ydbl_match_workspace(2, 300, 10, 10) == 4 * (100 + 1200) + 16
 
 
 def test_workspace_queries():

@@ -146,7 +146,8 @@ def test_predict_api(golden_dir):
 def _cpu_map50(o, x, labels):
     """mAP@0.5 of the CPU oracle path under the same val protocol (multi-label NMS, conf .001)."""
     from oracle.ops import clip_boxes, non_max_suppression
-    from ydbl.utils.metrics import IOUV, DetMetrics, box_iou, match_predictions
+    from oracle.metrics import IOUV, box_iou, match_predictions
+    from ydbl.utils.metrics import DetMetrics
 
     with torch.no_grad():
         y, _ = o(x)

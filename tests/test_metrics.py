@@ -6,7 +6,7 @@ import torch
 
 
 def test_box_iou_known_values():
-    from ydbl.utils.metrics import box_iou
+    from oracle.metrics import box_iou
 
     a = torch.tensor([[0.0, 0.0, 10.0, 10.0]])
     b = torch.tensor([[0.0, 0.0, 10.0, 10.0], [5.0, 0.0, 15.0, 10.0], [20.0, 20.0, 30.0, 30.0]])
@@ -28,7 +28,7 @@ def test_compute_ap_perfect_and_half():
 
 
 def test_match_predictions_greedy_unique():
-    from ydbl.utils.metrics import IOUV, box_iou, match_predictions
+    from oracle.metrics import IOUV, box_iou, match_predictions
 
     gt = torch.tensor([[0.0, 0.0, 10.0, 10.0]])
     gcls = torch.tensor([1.0])
@@ -50,3 +50,20 @@ def test_ap_per_class_two_classes():
     *_, ap, classes = ap_per_class(tp, conf, pred_cls, target_cls)
     assert list(classes) == [0, 1]
     assert abs(ap[0, 0] - 0.995) < 1e-6 and abs(ap[1, 0] - 0.995) < 1e-6
+
+
+def test_match_predictions_exact_tie_takes_larger_label():
+    """The rule ydbl_match_predictions restates for exact IoU ties (numpy's reversed stable argsort on
+    small match arrays): the detection matches the larger label index.  det0 overlaps both labels with
+    IoU exactly 0.6 and takes label 1, which leaves label 0 to det1."""
+    from oracle.metrics import IOUV, box_iou, match_predictions
+
+    gt = torch.tensor([[0.0, 0.0, 10.0, 10.0], [5.0, 0.0, 15.0, 10.0]])
+    gcls = torch.tensor([1.0, 1.0])
+    pred = torch.tensor([[2.5, 0.0, 12.5, 10.0], [0.0, 0.0, 10.0, 10.0]])
+    pcls = torch.tensor([1.0, 1.0])
+    iou = box_iou(gt, pred)
+    assert iou[0, 0] == iou[1, 0]
+    tp = match_predictions(pcls, gcls, iou, IOUV)
+    assert tp[0, :3].all() and not tp[0, 3:].any()
+    assert tp[1].all()

@@ -77,6 +77,18 @@ class NmsDesc(C.Structure):
                 ("out_count", C.c_void_p), ("workspace", C.c_void_p)]
 
 
+class LetterboxDesc(C.Structure):
+    _fields_ = [("src", C.c_void_p), ("src_off", C.c_void_p), ("meta", C.c_void_p), ("n", C.c_int32),
+                ("out_h", C.c_int32), ("out_w", C.c_int32), ("pad_value", C.c_float), ("out", C.c_void_p)]
+
+
+class MatchDesc(C.Structure):
+    _fields_ = [("det", C.c_void_p), ("det_count", C.c_void_p), ("n", C.c_int32), ("max_det", C.c_int32),
+                ("gt_box", C.c_void_p), ("gt_cls", C.c_void_p), ("gt_ofs", C.c_void_p), ("n_gt", C.c_int32),
+                ("iouv", C.c_void_p), ("n_iou", C.c_int32), ("single_cls", C.c_int32), ("correct", C.c_void_p),
+                ("workspace", C.c_void_p)]
+
+
 # name -> (argtypes, restype); every entry must exist in include/ydbl.h
 _P = C.c_void_p
 _VP = C.POINTER(View)
@@ -99,6 +111,9 @@ SIGNATURES = {
     "ydbl_pred_candidates": ([C.POINTER(PredCandDesc), _P], C.c_int),
     "ydbl_nms_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_nms": ([C.POINTER(NmsDesc), _P], C.c_int),
+    "ydbl_letterbox": ([C.POINTER(LetterboxDesc), _P], C.c_int),
+    "ydbl_match_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_match_predictions": ([C.POINTER(MatchDesc), _P], C.c_int),
     "ydbl_last_error": ([], C.c_char_p),
     "ydbl_version": ([], C.c_char_p),
 }

@@ -15,6 +15,7 @@ from __future__ import annotations
 import time
 from pathlib import Path
 
+import numpy as np
 import torch
 
 from ..nn.tasks import DetectionModel
@@ -22,7 +23,7 @@ from .results import Results
 from .session import DetectSession
 
 DEFAULTS = {"conf": 0.25, "iou": 0.7, "max_det": 300, "half": False, "fp8": False, "device": None, "agnostic_nms": False,
-            "classes": None, "batch": 1, "verbose": False}
+            "classes": None, "batch": 1, "verbose": False, "imgsz": 640}
 
 
 def select_device(device=None) -> torch.device:
@@ -123,25 +124,32 @@ class Model:
 
     # ------------------------------------------------------------------ inference
     def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
-                multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False) -> DetectSession:
+                multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True) -> DetectSession:
         dev = select_device(device)
         dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
-               bool(fp8))
+               bool(fp8), bool(clip))
         s = self._sessions.get(key)
         if s is None:
             with torch.cuda.device(dev):
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
-                                  keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8)
+                                  keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip)
             self._sessions[key] = s
         return s
 
     def predict(self, source=None, stream=False, **kwargs):
-        """U/engine/model.py:501-560 + DetectionPredictor.postprocess (U/models/yolo/detect/predict.py:23-41)."""
+        """U/engine/model.py:501-560 + DetectionPredictor.postprocess (U/models/yolo/detect/predict.py:23-41).
+
+        source: BCHW float tensor (LoadTensor rules), or HWC uint8 BGR ndarray frame(s), which are
+        letterboxed to imgsz on the GPU and whose boxes come back in frame coordinates.
+        """
         args = {**DEFAULTS, **self.overrides, **kwargs}
         dev = select_device(args["device"])
         t0 = time.perf_counter()
+        if isinstance(source, np.ndarray) or (isinstance(source, (list, tuple)) and source
+                                               and isinstance(source[0], np.ndarray)):
+            return self._predict_frames(source, args, dev, t0, stream)
         im = load_tensor_source(source, int(self.model.stride.max()))
         im = im.to(dev, non_blocking=True).float()
         b, _, h, w = im.shape
@@ -154,6 +162,35 @@ class Model:
         speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b, "postprocess": 0.0}
         results = [Results(im[i].permute(1, 2, 0), path=f"image{i}.jpg", names=self.model.names,
                            boxes=det[i, : counts[i]].clone(), speed=speed) for i in range(b)]
+        return iter(results) if stream else results
+
+    def _predict_frames(self, frames, args, dev, t0, stream):
+        from .preprocess import letterbox_batch, scale_boxes
+
+        frames = [frames] if isinstance(frames, np.ndarray) and frames.ndim == 3 else list(frames)
+        imgsz = args["imgsz"]
+        imgsz = (imgsz, imgsz) if isinstance(imgsz, int) else tuple(imgsz)
+        stride = int(self.model.stride.max())
+        im = letterbox_batch(frames, imgsz, stride=stride, device=dev)
+        b, _, h, w = im.shape
+        # the reference's NMS does not clip: boxes are clipped to the frame by scale_boxes
+        s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
+                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
+                         clip=False)
+        t1 = time.perf_counter()
+        det, cnt = s(im)
+        counts = cnt.tolist()
+        t2 = time.perf_counter()
+        results = []
+        for i, f in enumerate(frames):
+            boxes = det[i, : counts[i]].clone()
+            scale_boxes((h, w), boxes, f.shape[:2])
+            results.append(Results(f, path=f"image{i}.jpg", names=self.model.names, boxes=boxes))
+        t3 = time.perf_counter()
+        speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b,
+                 "postprocess": (t3 - t2) * 1e3 / b}
+        for r in results:
+            r.speed = speed
         return iter(results) if stream else results
 
     __call__ = predict
