@@ -75,15 +75,29 @@ class Model:
         self._sessions = {}
         model = str(model)
         suffix = Path(model).suffix.lower()
-        if suffix in (".pt", ".pth", ".safetensors"):
-            raise ValueError("build from a config and call .load(weights): YOLO('yolov13n_DBL.yaml').load('w.pt')")
-        self.model = DetectionModel(model, nc=nc, verbose=verbose)
+        if suffix in (".pt", ".pth"):
+            # reference checkpoint: build from its embedded yaml, then load its weights (U/nn/tasks.py:921-944)
+            from ..utils.checkpoint import read_reference_checkpoint
+
+            ck = read_reference_checkpoint(model)
+            if ck["yaml"] is None:
+                raise ValueError(f"{model} has no embedded model yaml: build from a config and call .load()")
+            self.model = DetectionModel(ck["yaml"], nc=nc, verbose=verbose)
+            self._load_sd(ck["state_dict"])
+            if ck["names"]:
+                self.model.names = ck["names"]
+            self.ckpt_path = model
+        elif suffix == ".safetensors":
+            raise ValueError("build from a config and call .load(weights): YOLO('yolov13n_DBL.yaml').load('w.safetensors')")
+        else:
+            self.model = DetectionModel(model, nc=nc, verbose=verbose)
         self.cfg = model
         self.overrides["model"] = model
 
     # ------------------------------------------------------------------ weights
     def load(self, weights):
         """Load a state_dict (torch weights_only file, safetensors, or a dict) with the reference's key names."""
+        names = None
         if isinstance(weights, dict):
             sd = weights
         elif str(weights).endswith(".safetensors"):
@@ -91,17 +105,23 @@ class Model:
 
             sd = load_file(str(weights))
         else:
-            obj = torch.load(str(weights), map_location="cpu", weights_only=True)
-            sd = obj.get("state_dict", obj.get("model", obj)) if isinstance(obj, dict) else obj
-            if not isinstance(sd, dict):
-                raise ValueError("weights file must hold a state_dict")
+            # plain state_dict files and the reference trainer's checkpoints, both without executing code
+            from ..utils.checkpoint import read_reference_checkpoint
+
+            ck = read_reference_checkpoint(weights)
+            sd, names = ck["state_dict"], ck["names"]
+        self._load_sd(sd)
+        if names:
+            self.model.names = names
+        self.ckpt_path = str(weights) if not isinstance(weights, dict) else None
+        return self
+
+    def _load_sd(self, sd):
         sd = {k[len("model."):] if k.startswith("model.model.") else k: v for k, v in sd.items()}
         missing, unexpected = self.model.load_state_dict(sd, strict=False)
         if unexpected:
             raise KeyError(f"unexpected keys in weights: {unexpected[:5]} ...")
         self._sessions.clear()
-        self.ckpt_path = str(weights) if not isinstance(weights, dict) else None
-        return self
 
     def state_dict(self):
         return self.model.state_dict()
