@@ -67,3 +67,30 @@ def test_match_predictions_exact_tie_takes_larger_label():
     tp = match_predictions(pcls, gcls, iou, IOUV)
     assert tp[0, :3].all() and not tp[0, 3:].any()
     assert tp[1].all()
+
+
+def test_results_host_api(tmp_path):
+    """Results/Boxes host API (U/engine/results.py): indexing, update+clip, save_txt, json/df, plot."""
+    import json
+
+    from ydbl.engine.results import Results
+
+    img = np.zeros((100, 200, 3), dtype=np.uint8)
+    data = torch.tensor([[10.0, 20.0, 60.0, 80.0, 0.9, 1.0], [150.0, 10.0, 190.0, 50.0, 0.5, 0.0]])
+    r = Results(img, "a.jpg", {0: "cat", 1: "dog"}, boxes=data)
+    assert len(r) == 2 and len(r[0]) == 1 and r[1].boxes.conf.item() == 0.5
+    assert r.verbose() == "1 cat, 1 dog, "
+    out = tmp_path / "labels" / "a.txt"
+    r.save_txt(out, save_conf=True)
+    lines = out.read_text().splitlines()
+    assert lines[0] == "1 0.175 0.5 0.25 0.6 0.9"
+    js = json.loads(r.to_json())
+    assert js[0]["name"] == "dog" and js[1]["box"]["x2"] == 190.0
+    assert list(r.to_df().columns) == ["name", "class", "confidence", "box"]
+    r.update(boxes=torch.tensor([[-5.0, -5.0, 250.0, 120.0, 0.7, 0.0]]))
+    assert r.boxes.xyxy.tolist() == [[0.0, 0.0, 200.0, 100.0]]
+    pic = r.plot()
+    assert pic.shape == img.shape and pic.dtype == np.uint8 and pic.any()
+    # the box outline uses the palette colour of class 0 (#042AFF, BGR (255, 42, 4))
+    assert tuple(pic[50, 0]) == (255, 42, 4)
+    assert r.numpy().boxes.data.shape == (1, 6)

@@ -2,13 +2,42 @@
 
 ``Boxes.data`` is ``[n, 6] = x1, y1, x2, y2, conf, cls`` exactly as the
 reference builds it in DetectionPredictor.postprocess
-(U/models/yolo/detect/predict.py:23-41).
+(U/models/yolo/detect/predict.py:23-41).  Host-side API of the reference's Results for detection:
+indexing, device moves, update (with clip_boxes), verbose, summary, save_txt, to_df / to_csv /
+to_json, and plot (boxes + labels drawn with PIL instead of the reference's cv2/PIL Annotator;
+same palette, not pixel-identical).
 """
 
 from __future__ import annotations
 
+import json
+from pathlib import Path
+
 import numpy as np
 import torch
+
+# U/utils/plotting.py Colors.hexs (the 20-colour detection palette), RGB
+_PALETTE = ["042AFF", "0BDBEB", "F3F3F3", "00DFB7", "111F68", "FF6FDD", "FF444F", "CCED00", "00F344", "BD00FF",
+            "00B4FF", "DD00BA", "00FFFF", "26C000", "01FFB3", "7D24FF", "7B0068", "FF1B6C", "FC6D2F", "A2FF0B"]
+
+
+def _color(i: int, bgr: bool = False):
+    h = _PALETTE[int(i) % len(_PALETTE)]
+    c = tuple(int(h[k:k + 2], 16) for k in (0, 2, 4))
+    return c[::-1] if bgr else c
+
+
+def _clip_boxes(boxes, shape):
+    """U/utils/ops.py:319-338."""
+    if isinstance(boxes, torch.Tensor):
+        boxes[..., 0] = boxes[..., 0].clamp(0, shape[1])
+        boxes[..., 1] = boxes[..., 1].clamp(0, shape[0])
+        boxes[..., 2] = boxes[..., 2].clamp(0, shape[1])
+        boxes[..., 3] = boxes[..., 3].clamp(0, shape[0])
+    else:
+        boxes[..., [0, 2]] = boxes[..., [0, 2]].clip(0, shape[1])
+        boxes[..., [1, 3]] = boxes[..., [1, 3]].clip(0, shape[0])
+    return boxes
 
 
 class Boxes:
@@ -103,15 +132,100 @@ class Results:
     def __len__(self):
         return 0 if self.boxes is None else len(self.boxes)
 
-    def cpu(self):
-        r = Results(self.orig_img, self.path, self.names, None, self.speed)
-        r.boxes = self.boxes.cpu() if self.boxes is not None else None
+    def __getitem__(self, idx):
+        return self._apply("__getitem__", idx)
+
+    def _apply(self, fn, *args, **kwargs):
+        r = self.new()
+        if self.boxes is not None:
+            r.boxes = getattr(self.boxes, fn)(*args, **kwargs)
         return r
 
+    def new(self):
+        return Results(self.orig_img, self.path, self.names, None, self.speed)
+
+    def update(self, boxes=None):
+        """U/engine/results.py:308-334 (boxes): clip to the original image and replace."""
+        if boxes is not None:
+            self.boxes = Boxes(_clip_boxes(boxes, self.orig_shape), self.orig_shape)
+
+    def cpu(self):
+        return self._apply("cpu")
+
     def numpy(self):
-        r = Results(self.orig_img, self.path, self.names, None, self.speed)
-        r.boxes = self.boxes.numpy() if self.boxes is not None else None
-        return r
+        return self._apply("numpy")
+
+    def cuda(self):
+        return self._apply("cuda")
+
+    def to(self, *args, **kwargs):
+        return self._apply("to", *args, **kwargs)
+
+    def save_txt(self, txt_file, save_conf=False):
+        """U/engine/results.py:665-718 (detection): 'cls xc yc w h [conf]' normalized, appended."""
+        texts = []
+        if self.boxes is not None and len(self.boxes):
+            b = self.boxes.cpu() if isinstance(self.boxes.data, torch.Tensor) else self.boxes
+            xywhn = torch.as_tensor(b.xywhn)
+            for j in range(len(b)):
+                d = b[j]
+                c, conf = int(torch.as_tensor(d.cls).item()), float(torch.as_tensor(d.conf).item())
+                tid = None if d.id is None else int(torch.as_tensor(d.id).item())
+                line = (c, *xywhn[j].view(-1).tolist()) + (conf,) * save_conf + (() if tid is None else (tid,))
+                texts.append(("%g " * len(line)).rstrip() % line)
+        if texts:
+            Path(txt_file).parent.mkdir(parents=True, exist_ok=True)
+            with open(txt_file, "a") as f:
+                f.writelines(t + "\n" for t in texts)
+        return str(txt_file)
+
+    def to_df(self, normalize=False, decimals=5):
+        import pandas as pd
+
+        return pd.DataFrame(self.summary(normalize=normalize, decimals=decimals))
+
+    def to_csv(self, normalize=False, decimals=5, *args, **kwargs):
+        return self.to_df(normalize=normalize, decimals=decimals).to_csv(*args, **kwargs)
+
+    def to_json(self, normalize=False, decimals=5):
+        return json.dumps(self.summary(normalize=normalize, decimals=decimals), indent=2)
+
+    def plot(self, conf=True, line_width=None, labels=True, boxes=True, img=None):
+        """Annotated copy of the original image (HWC uint8 BGR ndarray, like the reference's plot())."""
+        from PIL import Image, ImageDraw
+
+        im = self.orig_img if img is None else img
+        if isinstance(im, torch.Tensor):  # CHW/HWC float 0..1 tensor source -> HWC uint8 BGR
+            t = im.detach().float().cpu()
+            if t.ndim == 3 and t.shape[0] == 3 and t.shape[-1] != 3:
+                t = t.permute(1, 2, 0)
+            im = (t.clamp(0, 1) * 255).round().byte().numpy()[..., ::-1]
+        im = np.ascontiguousarray(im)
+        pil = Image.fromarray(im[..., ::-1].copy())  # BGR -> RGB for PIL
+        draw = ImageDraw.Draw(pil)
+        lw = line_width or max(round(sum(im.shape[:2]) / 2 * 0.003), 2)
+        if boxes and self.boxes is not None:
+            data = torch.as_tensor(self.boxes.data).detach().cpu()
+            for row in reversed(data.tolist()):
+                x1, y1, x2, y2, cf, c = row[0], row[1], row[2], row[3], row[-2], int(row[-1])
+                col = _color(c)
+                draw.rectangle([x1, y1, x2, y2], outline=col, width=lw)
+                if labels:
+                    name = self.names[c] if self.names else str(c)
+                    text = f"{name} {cf:.2f}" if conf else name
+                    tb = draw.textbbox((x1, y1), text)
+                    th = tb[3] - tb[1]
+                    ty = y1 - th - 2 if y1 - th - 2 >= 0 else y1
+                    draw.rectangle([x1, ty, x1 + (tb[2] - tb[0]) + 2, ty + th + 2], fill=col)
+                    draw.text((x1 + 1, ty), text, fill=(255, 255, 255))
+        return np.ascontiguousarray(np.asarray(pil)[..., ::-1])
+
+    def save(self, filename=None, **kwargs):
+        from PIL import Image
+
+        filename = filename or f"results_{Path(self.path).name}"
+        Image.fromarray(self.plot(**kwargs)[..., ::-1].copy()).save(filename)
+        return filename
 
     def summary(self, normalize=False, decimals=5):
         out = []
@@ -127,6 +241,7 @@ class Results:
         return out
 
     def verbose(self):
+        """U/engine/results.py:630-663 (detection)."""
         if self.boxes is None or len(self.boxes) == 0:
             return "(no detections), "
         cls = self.boxes.cls.int().tolist() if isinstance(self.boxes.cls, torch.Tensor) else list(self.boxes.cls)
