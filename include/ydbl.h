@@ -30,6 +30,8 @@
  *   ydbl_input_nchw_to_nhwc<- BasePredictor.preprocess engine/predictor.py:116-134 (+ LoadTensor /255)
  *   ydbl_conv_stem         <- preprocess (predictor.py:116-134) fused with the first backbone Conv
  *                             (conv.py:39-63 after fuse), reading the NCHW fp32 batch directly
+ *   ydbl_conv_stem2        <- preprocess + the backbone's first two Convs (layers 0-1 of the DBL yamls:
+ *                             Conv(3,C0,3,1) -> Conv(C0,2*C0,3,2), conv.py:39-63 after fuse), fp16
  *   ydbl_gate_add          <- FullPAD_Tunnel.forward nn/modules/block.py:1954-1956
  *   ydbl_pool_up_concat    <- FuseModule.forward block.py:1831-1840, DownsampleConv block.py:1927
  *   ydbl_dysample          <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
@@ -231,6 +233,23 @@ typedef struct {
 } ydbl_nms_desc;
 int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms);
 int ydbl_nms(const ydbl_nms_desc* d, void* stream);
+
+/* Stem pair (fp16): y = SiLU(conv3x3_s2(SiLU(conv3x3_s1(x * scale) + b0)) + b1), NHWC [n][ceil(h/2)][ceil(w/2)][2*c0],
+ * from the NCHW fp32 batch x [n][3][h][w]; the full-resolution intermediate never leaves LDS.
+ * params: device blob of ydbl_conv_stem2_params_size(c0) bytes filled on the HOST by
+ * ydbl_conv_stem2_pack from fp32 weights w0 [c0][3][3][3], b0 [c0], w1 [2*c0][c0][3][3], b1 [2*c0]
+ * (BN already folded); c0 = 8 or 16. */
+typedef struct {
+  const float* x;
+  int32_t n, cin, h, w;
+  float scale;
+  int32_t c0;
+  const void* params;
+  ydbl_view y;
+} ydbl_stem2_desc;
+int64_t ydbl_conv_stem2_params_size(int32_t c0);
+int ydbl_conv_stem2_pack(const float* w0, const float* b0, const float* w1, const float* b1, int32_t c0, void* out);
+int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream);
 
 /* LetterBox a batch of HWC uint8 BGR frames into one fp32 NCHW RGB canvas batch (values /255).
  * src: frames back to back, frame i at src + src_off[i] (int64 device array);

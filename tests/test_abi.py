@@ -42,6 +42,7 @@ STRUCTS = {
     "ydbl_nms_desc": "NmsDesc",
     "ydbl_match_desc": "MatchDesc",
     "ydbl_letterbox_desc": "LetterboxDesc",
+    "ydbl_stem2_desc": "Stem2Desc",
 }
 
 

@@ -320,6 +320,36 @@ def test_stem(dtype, cout, s, h, w):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
 
 
+@pytest.mark.parametrize("c0,n,h,w", [(8, 2, 64, 64), (16, 2, 37, 53), (8, 1, 640, 640), (16, 3, 17, 100),
+                                       (8, 2, 3, 5), (16, 1, 256, 320)])
+def test_stem2(c0, n, h, w):
+    """ydbl_conv_stem2 (preprocess + Conv s1 + Conv s2, fp16) vs the two convs in fp32 on fp16-rounded
+    operands, the intermediate rounded to fp16 as the unfused path stores it."""
+    from ydbl import _lib
+
+    torch.manual_seed(c0 + h)
+    x = torch.rand(n, 3, h, w)
+    w0 = torch.randn(c0, 3, 3, 3) / 27 ** 0.5
+    b0 = torch.randn(c0) * 0.5
+    w1 = torch.randn(2 * c0, c0, 3, 3) / (9 * c0) ** 0.5
+    b1 = torch.randn(2 * c0) * 0.5
+    h16 = lambda t: t.half().float()
+    mid = h16(F.silu(F.conv2d(h16(x), h16(w0), b0, 1, 1)))
+    ref = F.silu(F.conv2d(mid, h16(w1), b1, 2, 1))
+    plan = _plan(torch.float16)
+    ho, wo = ref.shape[2:]
+    yv = plan.alloc(n, ho, wo, 2 * c0, cs=2 * c0 + 8)  # channel stride wider than c (concat slice)
+    host = torch.empty(int(_lib.lib.ydbl_conv_stem2_params_size(c0)), dtype=torch.uint8)
+    _lib.check(_lib.lib.ydbl_conv_stem2_pack(w0.data_ptr(), b0.data_ptr(), w1.data_ptr(), b1.data_ptr(), c0,
+                                             host.data_ptr()))
+    params = host.to(DEV)
+    xd = x.to(DEV)
+    d = _lib.Stem2Desc(xd.data_ptr(), n, 3, h, w, 1.0, c0, params.data_ptr(), yv.struct())
+    plan.launch("ydbl_conv_stem2", d)
+    _run(plan)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, rtol=1e-2, atol=1e-2)
+
+
 def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False):
     """Run oracle module (CPU fp32) and product module (GPU) on the same inputs/weights."""
     p_mod.load_state_dict(o_mod.state_dict())

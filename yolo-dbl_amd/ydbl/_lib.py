@@ -77,6 +77,11 @@ class NmsDesc(C.Structure):
                 ("out_count", C.c_void_p), ("workspace", C.c_void_p)]
 
 
+class Stem2Desc(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("n", C.c_int32), ("cin", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
+                ("scale", C.c_float), ("c0", C.c_int32), ("params", C.c_void_p), ("y", View)]
+
+
 class LetterboxDesc(C.Structure):
     _fields_ = [("src", C.c_void_p), ("src_off", C.c_void_p), ("meta", C.c_void_p), ("n", C.c_int32),
                 ("out_h", C.c_int32), ("out_w", C.c_int32), ("pad_value", C.c_float), ("out", C.c_void_p)]
@@ -111,6 +116,9 @@ SIGNATURES = {
     "ydbl_pred_candidates": ([C.POINTER(PredCandDesc), _P], C.c_int),
     "ydbl_nms_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_nms": ([C.POINTER(NmsDesc), _P], C.c_int),
+    "ydbl_conv_stem2_params_size": ([C.c_int32], C.c_int64),
+    "ydbl_conv_stem2_pack": ([_P, _P, _P, _P, C.c_int32, _P], C.c_int),
+    "ydbl_conv_stem2": ([C.POINTER(Stem2Desc), _P], C.c_int),
     "ydbl_letterbox": ([C.POINTER(LetterboxDesc), _P], C.c_int),
     "ydbl_match_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_match_predictions": ([C.POINTER(MatchDesc), _P], C.c_int),

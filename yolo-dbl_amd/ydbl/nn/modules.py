@@ -194,6 +194,36 @@ def emit_stem(m: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: i
     return y
 
 
+def stem2_ok(m0, m1, ch: int, dtype) -> bool:
+    """Layers 0-1 can run as ydbl_conv_stem2: Conv(3, C0, 3, 1) + Conv(C0, 2*C0, 3, 2), SiLU, fp16, C0 in {8, 16}."""
+    if dtype != torch.float16 or not stem_ok(m0, ch) or type(m1) is not Conv:
+        return False
+    a, b = m0.conv, m1.conv
+    return (a.stride == (1, 1) and a.out_channels in (8, 16) and isinstance(m0.act, nn.SiLU)
+            and isinstance(m1.act, nn.SiLU) and b.groups == 1 and b.in_channels == a.out_channels
+            and b.out_channels == 2 * a.out_channels and b.kernel_size == (3, 3) and b.stride == (2, 2)
+            and b.padding == (1, 1) and b.dilation == (1, 1) and m1.f == -1)
+
+
+def emit_stem2(m0: "Conv", m1: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: int, w: int,
+               out: TV | None = None) -> TV:
+    """preprocess + layers 0 and 1 (conv.py:39-63, BN folded) in one kernel; layer 0's map stays in LDS."""
+    w0, b0 = m0.folded()
+    w1, b1 = m1.folded()
+    c0 = m0.conv.out_channels
+    ho, wo = conv_out_hw(h, w, 3, 2, 1, 1)
+    y = out if out is not None else plan.alloc(n, ho, wo, 2 * c0)
+    b0 = b0 if b0 is not None else torch.zeros(c0)
+    b1 = b1 if b1 is not None else torch.zeros(2 * c0)
+    host = torch.empty(int(_lib.lib.ydbl_conv_stem2_params_size(c0)), dtype=torch.uint8)
+    args = [t.float().contiguous() for t in (w0, b0, w1, b1)]
+    _lib.check(_lib.lib.ydbl_conv_stem2_pack(*[t.data_ptr() for t in args], c0, host.data_ptr()), "ydbl_conv_stem2_pack")
+    params = plan.const(host)
+    d = _lib.Stem2Desc(x_nchw.data_ptr(), n, ch, h, w, 1.0, c0, params.data_ptr(), y.struct())
+    plan.launch("ydbl_conv_stem2", d, what="Stem.conv3x3x2", keep=[params, d])
+    return y
+
+
 def emit_seq(plan: Plan, mods, x, out=None):
     mods = list(mods)
     for i, m in enumerate(mods):

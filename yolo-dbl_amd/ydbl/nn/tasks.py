@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import json
 import math
+import os
 import re
 from copy import deepcopy
 from pathlib import Path
@@ -222,10 +223,23 @@ class DetectionModel(nn.Module):
         y: list[TV | None] = []
         x = inp
         stem = layers[0] if M.stem_ok(layers[0], self.yaml["ch"]) and 0 not in out_hint else None
+        # layers 0+1 as one kernel when layer 0's map feeds layer 1 only (the full-resolution map never
+        # reaches HBM); YDBL_NO_STEM2=1 keeps them separate (A/B switch)
+        used_later = any(j == 0 for m in layers[2:] for j in ([m.f] if isinstance(m.f, int) else m.f))
+        stem2 = (stem is not None and len(layers) > 1 and not used_later and not os.environ.get("YDBL_NO_STEM2")
+                 and M.stem2_ok(layers[0], layers[1], self.yaml["ch"], dtype))
         if stem is None:
             plan.launch("ydbl_input_nchw_to_nhwc", x_nchw.data_ptr(), batch, self.yaml["ch"], h, w, 1.0, inp.struct(),
                         what="input")
         for m in layers:
+            if stem2 and m is layers[1]:
+                y.append(x)
+                continue
+            if m is stem and stem2:  # preprocess + layers 0 and 1 in one kernel
+                x = M.emit_stem2(layers[0], layers[1], plan, x_nchw, batch, self.yaml["ch"], h, w,
+                                 cat_buf.get(1, out_hint.get(1)))
+                y.append(None)  # layer 0's map is never materialised
+                continue
             if m is stem:  # preprocess + first Conv fused, straight from the NCHW batch
                 x = M.emit_stem(m, plan, x_nchw, batch, self.yaml["ch"], h, w)
                 y.append(x)
