@@ -199,6 +199,7 @@ def main():
     images = B * world * args.steps
     value = images / el
     dets_per_img = float(sess.count.float().mean().item())
+    cands_per_img = float(sess.cand_count.float().mean().item())
 
     rf = None
     if rank == 0 and not args.no_roofline:
@@ -225,6 +226,7 @@ def main():
                        "model": Path(cfg).stem, "global_batch": B * world, "imgsz": S, "nc": 3,
                        "parallelism": f"dp{world}"},
             "dets_per_image": round(dets_per_img, 2),
+            "candidates_per_image": round(cands_per_img, 1),
             "roofline": rf,
             "cpu_baseline": cpu,
         }

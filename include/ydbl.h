@@ -30,6 +30,8 @@
  *   ydbl_input_nchw_to_nhwc<- BasePredictor.preprocess engine/predictor.py:116-134 (+ LoadTensor /255)
  *   ydbl_conv_stem         <- preprocess (predictor.py:116-134) fused with the first backbone Conv
  *                             (conv.py:39-63 after fuse), reading the NCHW fp32 batch directly
+ *   ydbl_bottleneck_nhwc   <- Bottleneck.forward nn/modules/block.py:355-357 (cv1 -> cv2 [+ x], both
+ *                             Conv = conv.py:39-63 after fuse) as one kernel
  *   ydbl_conv_stem2        <- preprocess + the backbone's first two Convs (layers 0-1 of the DBL yamls:
  *                             Conv(3,C0,3,1) -> Conv(C0,2*C0,3,2), conv.py:39-63 after fuse), fp16
  *   ydbl_gate_add          <- FullPAD_Tunnel.forward nn/modules/block.py:1954-1956
@@ -250,6 +252,23 @@ typedef struct {
 int64_t ydbl_conv_stem2_params_size(int32_t c0);
 int ydbl_conv_stem2_pack(const float* w0, const float* b0, const float* w1, const float* b1, int32_t c0, void* out);
 int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream);
+
+/* Fused Bottleneck (fp16): y = [x +] SiLU(conv3x3(SiLU(conv3x3(x) + b1)) + b2), c -> c/2 -> c channels,
+ * stride 1, pad 1 (Bottleneck(c, c, shortcut, e=0.5) with Conv = conv + folded BN + SiLU); the c/2
+ * intermediate never leaves LDS.  x, y: NHWC fp16 views of the same shape with x.c == y.c == c
+ * (c = 16, 32 or 64), y must not alias x.  params: device blob of ydbl_bottleneck_params_size(c)
+ * bytes filled on the HOST by ydbl_bottleneck_pack from fp32 w1 [c/2][c][3][3], b1 [c/2],
+ * w2 [c][c/2][3][3], b2 [c] (BN folded).  tile_h: 0 = auto, else 8 or 16 output rows per workgroup. */
+typedef struct {
+  ydbl_view x, y;
+  int32_t c;
+  int32_t add;
+  int32_t tile_h;
+  const void* params;
+} ydbl_bottleneck_desc;
+int64_t ydbl_bottleneck_params_size(int32_t c);
+int ydbl_bottleneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c, void* out);
+int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream);
 
 /* LetterBox a batch of HWC uint8 BGR frames into one fp32 NCHW RGB canvas batch (values /255).
  * src: frames back to back, frame i at src + src_off[i] (int64 device array);

@@ -43,6 +43,7 @@ STRUCTS = {
     "ydbl_match_desc": "MatchDesc",
     "ydbl_letterbox_desc": "LetterboxDesc",
     "ydbl_stem2_desc": "Stem2Desc",
+    "ydbl_bottleneck_desc": "BottleneckDesc",
 }
 
 

@@ -1,0 +1,325 @@
+// Fused Bottleneck (fp16): y = x + SiLU(conv3x3(SiLU(conv3x3(x) + b1)) + b2)   (add = shortcut && c1 == c2)
+// U/nn/modules/block.py:344-357 with Conv = conv + folded BN + SiLU (U/nn/modules/conv.py:39-63).
+//
+// The DBL backbones run chains of Bottleneck(C, C, e=0.5) at high resolution (DBL-n: C=16 @320^2,
+// 32 @160^2, 4x 64 @80^2).  As two launches the C/2-channel intermediate is written to HBM and read
+// back, and each 3x3 conv stages its own input; the pair is ~0.45 ms of DBL-n's 2.8 ms step.  Here a
+// workgroup owns a TH x 16 output tile and all C output channels:
+//   1. the (TH+4) x 20 input window, all C channels, is staged once in LDS (16-byte records, one plane
+//      per 8-channel chunk; the lane -> (pixel, chunk) order gives 1 KiB contiguous global reads per
+//      wave and conflict-free ds_write_b128 groups);
+//   2. cv1 over the (TH+2) x 18 intermediate window on MFMA 16x16x32 f16, walked as a virtual grid with
+//      the input's 20-record pitch (the two dead columns per row cost 11 %, and a lane's B address is
+//      its pixel index plus a per-k-step constant), + bias + SiLU, zero outside the image (cv2's
+//      padding), rounded to fp16 exactly as the unfused path stores it -> LDS;
+//   3. cv2 over the TH x 16 tile from that LDS window, + bias + SiLU, + x (read back from the staged
+//      input window), -> NHWC fp16.
+// Weights never touch LDS: each wave keeps the MFMA A fragments of its output-channel tile in VGPRs
+// (one 1 KiB coalesced load per k-step, every weight read once per workgroup).
+// K order per 32-wide k-step (lane group g = lane / 16 supplies k = 8g..8g+7): chosen per channel
+// count so that the two lane groups a ds_read_b128 services together ({g0, g1}, {g2, g3}) read from
+// addresses 256 B apart (same bank quad offset): for >= 32 channels a k-step is one tap x 4 chunks, for
+// 16 channels two taps x 2 chunks, for 8 channels four taps paired by equal dx (planes/pitches are
+// multiples of 16 records).  Pack (host) and kernel share kslot().
+// HBM traffic: x once (+ the 4-row halo, mostly L2 hits), y once; the intermediate never leaves LDS.
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace ydbl {
+
+struct KSlot {
+  int tap, chunk;
+  bool live;
+};
+
+// k-step m, lane group g -> (tap = dy*3 + dx, 8-channel chunk, live); dead slots carry zero weights
+// and point at a live address (finite data, broadcast reads)
+template <int CH>
+__host__ __device__ constexpr KSlot kslot(int m, int g) {
+  if constexpr (CH >= 4) {
+    return KSlot{m / (CH / 4), (m % (CH / 4)) * 4 + g, true};
+  } else if constexpr (CH == 2) {
+    const int tap = 2 * m + (g >> 1);
+    return KSlot{tap < 9 ? tap : 8, g & 1, tap < 9};
+  } else {
+    // {g0,g1} and {g2,g3} share dx: (0,0)(1,0)|(0,1)(1,1), (0,2)(1,2)|(2,0)(2,0)', (2,1)(2,1)'|(2,2)(2,2)'
+    constexpr int taps[3][4] = {{0, 3, 1, 4}, {2, 5, 6, 6}, {7, 7, 8, 8}};
+    constexpr bool live[3][4] = {{true, true, true, true}, {true, true, true, false}, {true, false, true, false}};
+    return KSlot{taps[m][g], 0, live[m][g]};
+  }
+}
+template <int CH>
+constexpr int ksteps() {
+  return CH >= 4 ? 9 * CH / 4 : (CH == 2 ? 5 : 3);
+}
+constexpr int rup16(int v) { return (v + 15) / 16 * 16; }
+
+template <int C, int TH>
+struct BneckCfg {
+  static constexpr int CM = C / 2, CH = C / 8, CHM = (CM + 7) / 8;
+  static constexpr int NT1 = (CM + 15) / 16, NT2 = C / 16;
+  static constexpr int KS1 = ksteps<CH>(), KS2 = ksteps<CHM>();
+  static constexpr int TW = 16;
+  static constexpr int IP = TW + 4;                  // input window pitch (records) = its width
+  static constexpr int IR = TH + 5;                  // + 1 slack row for the virtual grid's tail
+  static constexpr int NPX = IR * IP;
+  static constexpr int PIN = rup16(NPX);             // chunk plane, records (multiple of 16: 256 B)
+  static constexpr int MR = TH + 2;
+  static constexpr int MP = CHM == 1 ? 32 : IP;      // 8-channel intermediate: pitch a multiple of 16
+  static constexpr int PMID = rup16(MR * MP);
+  static constexpr int G1 = (MR * IP + 15) / 16;     // 16-pixel groups of the cv1 virtual grid
+  static constexpr int IN_BYTES = CH * PIN * 16, MID_BYTES = CHM * PMID * 16;
+  static constexpr int LDS = IN_BYTES + MID_BYTES;
+  static constexpr int W1F = NT1 * KS1 * 64, W2F = NT2 * KS2 * 64;  // h8 fragments
+  static constexpr int64_t BYTES = (int64_t)(W1F + W2F) * 16 + (NT1 * 16 + C) * 4;
+  static_assert(CH >= 2, "input needs >= 16 channels");
+  static_assert((G1 * 16 - 1) + 2 * IP + 2 < NPX, "virtual grid tail must stay inside the window");
+};
+
+// Host: fp32 PyTorch-layout weights (BN folded) -> fragment blob.  A[row][k]: row = output channel of
+// the 16-channel tile, k = 32m + 8g + j -> (kslot(m, g), channel chunk*8 + j).
+template <int C>
+void bneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, unsigned char* out) {
+  using Cfg = BneckCfg<C, 16>;
+  constexpr int CM = Cfg::CM;
+  _Float16* f1 = reinterpret_cast<_Float16*>(out);
+  _Float16* f2 = f1 + Cfg::W1F * 8;
+  float* fb1 = reinterpret_cast<float*>(f2 + Cfg::W2F * 8);
+  float* fb2 = fb1 + Cfg::NT1 * 16;
+  for (int t = 0; t < Cfg::NT1; ++t)
+    for (int m = 0; m < Cfg::KS1; ++m)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const KSlot s = kslot<Cfg::CH>(m, lane >> 4);
+          const int co = 16 * t + (lane & 15), ci = s.chunk * 8 + j;
+          const bool ok = s.live && co < CM;
+          f1[((t * Cfg::KS1 + m) * 64 + lane) * 8 + j] = (_Float16)(ok ? w1[(co * C + ci) * 9 + s.tap] : 0.f);
+        }
+  for (int t = 0; t < Cfg::NT2; ++t)
+    for (int m = 0; m < Cfg::KS2; ++m)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const KSlot s = kslot<Cfg::CHM>(m, lane >> 4);
+          const int co = 16 * t + (lane & 15), ci = s.chunk * 8 + j;
+          const bool ok = s.live && ci < CM;
+          f2[((t * Cfg::KS2 + m) * 64 + lane) * 8 + j] = (_Float16)(ok ? w2[(co * CM + ci) * 9 + s.tap] : 0.f);
+        }
+  for (int i = 0; i < Cfg::NT1 * 16; ++i) fb1[i] = i < CM ? b1[i] : 0.f;
+  for (int i = 0; i < C; ++i) fb2[i] = b2[i];
+}
+
+// per-k-step LDS byte offset of lane group g's slot relative to its pixel record (PL = chunk plane,
+// P = pitch, both in records); g-independent except for the lane base chunk when CH >= 4
+template <int CH, int PL, int P>
+__device__ __forceinline__ int koff(int m, int g) {
+  const KSlot s = kslot<CH>(m, CH >= 4 ? 0 : g);
+  return (s.chunk * PL + (s.tap / 3) * P + s.tap % 3) * 16;
+}
+template <int CH, int PL>
+__device__ __forceinline__ int kbase(int g) {
+  return CH >= 4 ? g * PL * 16 : 0;
+}
+
+template <int C, int TH, bool ADD>
+__global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, DView<_Float16> y,
+                                                       const unsigned char* __restrict__ params, int tiles_x,
+                                                       int tiles_y, int ntiles) {
+  using Cfg = BneckCfg<C, TH>;
+  constexpr int CH = Cfg::CH, CHM = Cfg::CHM, CM = Cfg::CM;
+  constexpr int IP = Cfg::IP, MP = Cfg::MP, PIN = Cfg::PIN, PMID = Cfg::PMID;
+  constexpr int NT1 = Cfg::NT1, NT2 = Cfg::NT2, KS1 = Cfg::KS1, KS2 = Cfg::KS2;
+  const h8* w1f = reinterpret_cast<const h8*>(params);
+  const h8* w2f = w1f + Cfg::W1F;
+  const float* b1 = reinterpret_cast<const float*>(w2f + Cfg::W2F);
+  const float* b2 = b1 + NT1 * 16;
+  __shared__ __align__(16) unsigned char smem[Cfg::LDS];
+  unsigned char* s_in = smem;                    // [CH][PIN] records
+  unsigned char* s_mid = smem + Cfg::IN_BYTES;   // [CHM][PMID] records
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int t = (ntiles & 7) ? (int)blockIdx.x : xcd_remap(blockIdx.x, ntiles);
+  const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y;
+  const int img = t / (tiles_x * tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * Cfg::TW;
+
+  // ---- 1. input window (image rows oy0-2.., cols ox0-2..).  Item i = u*256 + tid -> chunk
+  // (i >> 3) % CH (the same for every u: CH divides 32), pixel px0 + u * 256/CH: each wave reads
+  // 1 KiB of contiguous NHWC pixels per instruction, each 8-lane ds_write_b128 group 8 records
+  static_assert(32 % CH == 0, "staging pattern assumes CH | 32");
+  constexpr int PXU = 256 / CH;
+  constexpr int IT = (Cfg::NPX + PXU - 1) / PXU;
+  const int s_chunk = (tid >> 3) % CH, px0 = ((tid >> 3) / CH) * 8 + (tid & 7);
+  h8 xr[IT];
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int px = px0 + u * PXU;
+    const int r = px / IP, c = px - r * IP;
+    const int iy = oy0 - 2 + r, ix = ox0 - 2 + c;
+    const bool ok = px < Cfg::NPX && iy >= 0 && iy < x.h && ix >= 0 && ix < x.w;
+    const _Float16* src = ok ? x.at(img, iy, ix) + s_chunk * 8 : x.p;
+    const h8 v = *reinterpret_cast<const h8*>(src);
+    xr[u] = ok ? v : h8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  // this wave's weight tiles, VGPR-resident
+  const int t1 = wave % NT1, t2 = wave % NT2;
+  h8 a1[KS1], a2[KS2];
+#pragma unroll
+  for (int m = 0; m < KS1; ++m) a1[m] = w1f[(t1 * KS1 + m) * 64 + lane];
+#pragma unroll
+  for (int m = 0; m < KS2; ++m) a2[m] = w2f[(t2 * KS2 + m) * 64 + lane];
+  unsigned char* s_dst = s_in + (s_chunk * PIN + px0) * 16;
+#pragma unroll
+  for (int u = 0; u < IT; ++u)
+    if (px0 + u * PXU < Cfg::NPX) *reinterpret_cast<h8*>(s_dst + u * PXU * 16) = xr[u];
+  float bias1[4], bias2[4];
+  const int c1 = 16 * t1 + 4 * g;  // first intermediate channel of this lane's cv1 D rows
+  const int c2 = 16 * t2 + 4 * g;  // first output channel of this lane's cv2 D rows
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    bias1[q] = b1[c1 + q];
+    bias2[q] = b2[c2 + q];
+  }
+  unsigned char* mid_w = s_mid + ((c1 >> 3) * PMID) * 16 + (c1 & 7) * 2;
+  const unsigned char* in_b = s_in + kbase<CH, PIN>(g);
+  const bool interior = oy0 >= 1 && ox0 >= 1 && oy0 + TH + 1 <= y.h && ox0 + Cfg::TW + 1 <= y.w;
+  __syncthreads();
+
+  // ---- 2. cv1 over the virtual grid: MR rows x IP columns, mid pixel v reads input record v + tap.
+  // Two 16-pixel groups per iteration (independent accumulators: the LDS reads of one overlap the
+  // MFMAs of the other, and the two SiLU epilogues interleave)
+  auto epi1 = [&](const f32x4& acc, int v) {
+    const int vr = v / IP, vc = v - vr * IP;
+    if (vr >= Cfg::MR || c1 >= CM) return;
+    bool inside = true;
+    if (!interior) {
+      const int my = oy0 - 1 + vr, mx = ox0 - 1 + vc;
+      inside = my >= 0 && my < y.h && mx >= 0 && mx < y.w;
+    }
+    h4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (_Float16)(inside ? silu_fast(acc[q] + bias1[q]) : 0.f);
+    *reinterpret_cast<h4*>(mid_w + (vr * MP + vc) * 16) = o;
+  };
+  constexpr int WPT1 = 4 / NT1;
+  for (int gi = wave / NT1; gi < Cfg::G1; gi += 2 * WPT1) {
+    const int v0 = gi * 16 + r16;
+    const bool two = gi + WPT1 < Cfg::G1;  // wave-uniform
+    const int v1 = two ? v0 + 16 * WPT1 : v0;
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    const unsigned char* p0 = in_b + v0 * 16;
+    const unsigned char* p1 = in_b + v1 * 16;
+#pragma unroll
+    for (int m = 0; m < KS1; ++m) {
+      const int o = koff<CH, PIN, IP>(m, g);
+      const h8 bf0 = *reinterpret_cast<const h8*>(p0 + o);
+      const h8 bf1 = *reinterpret_cast<const h8*>(p1 + o);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf1, acc1, 0, 0, 0);
+    }
+    epi1(acc0, v0);
+    if (two) epi1(acc1, v1);
+  }
+
+  const unsigned char* res_r = s_in + ((c2 >> 3) * PIN + 2 * IP + 2) * 16 + (c2 & 7) * 2;
+  const unsigned char* mid_b = s_mid + kbase<CHM, PMID>(g);
+  __syncthreads();
+
+  // ---- 3. cv2: output rows j, j + WPT2 of the tile, 16 columns = the 16 lanes
+  auto epi2 = [&](const f32x4& acc, int j) {
+    const int oy = oy0 + j, ox = ox0 + r16;
+    if (oy >= y.h || ox >= y.w) return;
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = silu_fast(acc[q] + bias2[q]);
+    if constexpr (ADD) {
+      const h4 rv = *reinterpret_cast<const h4*>(res_r + (j * IP + r16) * 16);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = float(rv[q]) + v[q];
+    }
+    store_f<4>(y.at(img, oy, ox) + c2, v);
+  };
+  constexpr int WPT2 = 4 / NT2;
+  for (int j = wave / NT2; j < TH; j += 2 * WPT2) {
+    const bool two = j + WPT2 < TH;
+    const int j1 = two ? j + WPT2 : j;
+    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    const unsigned char* p0 = mid_b + (j * MP + r16) * 16;
+    const unsigned char* p1 = mid_b + (j1 * MP + r16) * 16;
+#pragma unroll
+    for (int m = 0; m < KS2; ++m) {
+      const int o = koff<CHM, PMID, MP>(m, g);
+      const h8 bf0 = *reinterpret_cast<const h8*>(p0 + o);
+      const h8 bf1 = *reinterpret_cast<const h8*>(p1 + o);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[m], bf0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[m], bf1, acc1, 0, 0, 0);
+    }
+    epi2(acc0, j);
+    if (two) epi2(acc1, j1);
+  }
+}
+
+}  // namespace ydbl
+
+using namespace ydbl;
+
+extern "C" int64_t ydbl_bottleneck_params_size(int32_t c) {
+  if (c == 16) return BneckCfg<16, 16>::BYTES;
+  if (c == 32) return BneckCfg<32, 16>::BYTES;
+  if (c == 64) return BneckCfg<64, 16>::BYTES;
+  return -1;
+}
+
+extern "C" int ydbl_bottleneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c,
+                                    void* out) {
+  if (!w1 || !b1 || !w2 || !b2 || !out) return fail(YDBL_EINVAL, "bottleneck_pack: null pointer");
+  auto* o = reinterpret_cast<unsigned char*>(out);
+  if (c == 16) { bneck_pack<16>(w1, b1, w2, b2, o); return 0; }
+  if (c == 32) { bneck_pack<32>(w1, b1, w2, b2, o); return 0; }
+  if (c == 64) { bneck_pack<64>(w1, b1, w2, b2, o); return 0; }
+  return fail(YDBL_EINVAL, "bottleneck_pack: c must be 16, 32 or 64");
+}
+
+template <int C, int TH>
+static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
+  using Cfg = BneckCfg<C, TH>;
+  const int tiles_x = (int)cdiv(d->y.w, Cfg::TW), tiles_y = (int)cdiv(d->y.h, TH);
+  const int64_t nt = (int64_t)tiles_x * tiles_y * d->y.n;
+  if (nt > 0x7fffffff) return fail(YDBL_EINVAL, "bottleneck: grid too large");
+  auto x = dview<const _Float16>(d->x);
+  auto y = dview<_Float16>(d->y);
+  auto* p = reinterpret_cast<const unsigned char*>(d->params);
+  if (d->add)
+    bneck_kernel<C, TH, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
+  else
+    bneck_kernel<C, TH, false><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
+  return check_launch("ydbl_bottleneck_nhwc");
+}
+
+template <int C>
+static int bneck_dispatch(const ydbl_bottleneck_desc* d, hipStream_t s) {
+  // 16-row tiles halve the halo recompute; 8-row tiles when 16-row ones leave the chip under-filled
+  const int64_t t16 = cdiv(d->y.h, 16) * cdiv(d->y.w, 16) * (int64_t)d->y.n;
+  const int th = d->tile_h ? d->tile_h : (t16 >= 1024 ? 16 : 8);
+  return th == 16 ? bneck_go<C, 16>(d, s) : bneck_go<C, 8>(d, s);
+}
+
+extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream) {
+  if (!d) return fail(YDBL_EINVAL, "bottleneck: null descriptor");
+  if (!d->params) return fail(YDBL_EINVAL, "bottleneck: null parameters");
+  if (check_view(&d->x, "bottleneck.x", true) || check_view(&d->y, "bottleneck.y", true)) return YDBL_EINVAL;
+  if (d->x.dtype != YDBL_F16 || d->y.dtype != YDBL_F16) return fail(YDBL_EINVAL, "bottleneck: fp16 views only");
+  const int c = d->c;
+  if (d->x.c != c || d->y.c != c) return fail(YDBL_EINVAL, "bottleneck: x.c and y.c must equal c");
+  if (d->x.n != d->y.n || d->x.h != d->y.h || d->x.w != d->y.w)
+    return fail(YDBL_EINVAL, "bottleneck: x and y shapes differ");
+  if (d->y.n < 1 || d->y.h < 1 || d->y.w < 1) return fail(YDBL_EINVAL, "bottleneck: empty input");
+  if (d->tile_h != 0 && d->tile_h != 8 && d->tile_h != 16) return fail(YDBL_EINVAL, "bottleneck: tile_h must be 0, 8 or 16");
+  if (d->x.ptr == d->y.ptr) return fail(YDBL_EINVAL, "bottleneck: in-place is not supported (halo reads)");
+  hipStream_t s = as_stream(stream);
+  if (c == 16) return bneck_dispatch<16>(d, s);
+  if (c == 32) return bneck_dispatch<32>(d, s);
+  if (c == 64) return bneck_dispatch<64>(d, s);
+  return fail(YDBL_EINVAL, "bottleneck: c must be 16, 32 or 64");
+}

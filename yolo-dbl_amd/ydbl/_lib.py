@@ -82,6 +82,11 @@ class Stem2Desc(C.Structure):
                 ("scale", C.c_float), ("c0", C.c_int32), ("params", C.c_void_p), ("y", View)]
 
 
+class BottleneckDesc(C.Structure):
+    _fields_ = [("x", View), ("y", View), ("c", C.c_int32), ("add", C.c_int32), ("tile_h", C.c_int32),
+                ("params", C.c_void_p)]
+
+
 class LetterboxDesc(C.Structure):
     _fields_ = [("src", C.c_void_p), ("src_off", C.c_void_p), ("meta", C.c_void_p), ("n", C.c_int32),
                 ("out_h", C.c_int32), ("out_w", C.c_int32), ("pad_value", C.c_float), ("out", C.c_void_p)]
@@ -119,6 +124,9 @@ SIGNATURES = {
     "ydbl_conv_stem2_params_size": ([C.c_int32], C.c_int64),
     "ydbl_conv_stem2_pack": ([_P, _P, _P, _P, C.c_int32, _P], C.c_int),
     "ydbl_conv_stem2": ([C.POINTER(Stem2Desc), _P], C.c_int),
+    "ydbl_bottleneck_params_size": ([C.c_int32], C.c_int64),
+    "ydbl_bottleneck_pack": ([_P, _P, _P, _P, C.c_int32, _P], C.c_int),
+    "ydbl_bottleneck_nhwc": ([C.POINTER(BottleneckDesc), _P], C.c_int),
     "ydbl_letterbox": ([C.POINTER(LetterboxDesc), _P], C.c_int),
     "ydbl_match_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_match_predictions": ([C.POINTER(MatchDesc), _P], C.c_int),

@@ -341,7 +341,29 @@ class Bottleneck(nn.Module):
         self.cv2 = Conv(c_, c2, k[1], 1, g=g)
         self.add = shortcut and c1 == c2
 
+    def fused_ok(self, plan, x) -> bool:
+        """cv1 -> cv2 as one ydbl_bottleneck_nhwc launch: fp16, c -> c/2 -> c, 3x3 s1 both, SiLU both."""
+        a, b = self.cv1.conv, self.cv2.conv
+        c = b.out_channels
+        return (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and c in (16, 32, 64)
+                and x.c == c == a.in_channels and a.out_channels == c // 2 == b.in_channels
+                and all(m.kernel_size == (3, 3) and m.stride == (1, 1) and m.padding == (1, 1)
+                        and m.dilation == (1, 1) and m.groups == 1 for m in (a, b))
+                and isinstance(self.cv1.act, nn.SiLU) and isinstance(self.cv2.act, nn.SiLU))
+
     def emit(self, plan, x, out=None):
+        if self.fused_ok(plan, x):
+            c = x.c
+            y = out if out is not None else plan.alloc(x.n, x.h, x.w, c)
+            if y.base is not x.base:  # the kernel reads a halo of x while writing y
+                args = [t.float().contiguous() for t in (*self.cv1.folded(), *self.cv2.folded())]
+                host = torch.empty(int(_lib.lib.ydbl_bottleneck_params_size(c)), dtype=torch.uint8)
+                _lib.check(_lib.lib.ydbl_bottleneck_pack(*[t.data_ptr() for t in args], c, host.data_ptr()),
+                           "ydbl_bottleneck_pack")
+                params = plan.const(host)
+                d = _lib.BottleneckDesc(x.struct(), y.struct(), c, int(self.add), 0, params.data_ptr())
+                plan.launch("ydbl_bottleneck_nhwc", d, what=f"Bottleneck.c{c}", keep=[params, d])
+                return y
         t = self.cv1.emit(plan, x)
         return self.cv2.emit(plan, t, out, res=x if self.add else None,
                              res_mode=_lib.RES_ADD if self.add else _lib.RES_NONE)
