@@ -200,6 +200,7 @@ def main():
     value = images / el
     dets_per_img = float(sess.count.float().mean().item())
     cands_per_img = float(sess.cand_count.float().mean().item())
+    cands_max = int(sess.cand_count.max().item())
 
     rf = None
     if rank == 0 and not args.no_roofline:
@@ -227,6 +228,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "dets_per_image": round(dets_per_img, 2),
             "candidates_per_image": round(cands_per_img, 1),
+            "candidates_max": cands_max,
             "roofline": rf,
             "cpu_baseline": cpu,
         }

@@ -206,16 +206,25 @@ __device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4
   const float ww = fmaxf(0.f, xx2 - xx1), hh = fmaxf(0.f, yy2 - yy1);
   const float inter = ww * hh;
   const float area_b = (b[2] - b[0]) * (b[3] - b[1]);
-  const float ovr = inter / ((area_a + area_b) - inter);
+  const float uni = (area_a + area_b) - inter;
+  // The decision is torchvision's: the correctly rounded fp32 quotient inter / uni, compared in
+  // double.  inter * rcp(uni) is within a few ulp of that quotient, so it decides alone unless it
+  // lies within 1e-5 (relative) of the threshold; only those cases pay for the IEEE division.
+  const float approx = inter * __builtin_amdgcn_rcpf(uni);
+  const double ad = (double)approx;
+  if (ad > thr * (1.0 + 1e-5) + 1e-30) return true;
+  if (ad < thr * (1.0 - 1e-5) - 1e-30) return false;
+  const float ovr = inter / uni;
   return (double)ovr > thr;
 }
 
 __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   // LDS: sort keys (64 KB) are reused for the first 4096 sorted boxes after sorting.
-  __shared__ uint64_t s_keys[NMS_SORT_LDS];
+  __shared__ __align__(16) uint64_t s_keys[NMS_SORT_LDS];
   __shared__ int s_vals[NMS_SORT_LDS];
   __shared__ unsigned char removed[NMS_MAX_FLAGS];
-  __shared__ int kept_sorted[NMS_MAX_DET];
+  __shared__ int kept_slot[NMS_MAX_DET];
+  __shared__ int s_wsum[NMS_THREADS / 64];
   __shared__ f32x4 chunk_box[64];
   __shared__ unsigned char cmask[64][16];
   __shared__ int s_nk;
@@ -230,7 +239,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   const bool in_lds = n <= NMS_SORT_LDS;
   int P = 64;
   while (P < n) P <<= 1;
-  const int* order;  // sorted position -> candidate slot
+  int* order;  // list position -> candidate slot
   if (in_lds) {
     for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
       s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
@@ -278,73 +287,141 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   __syncthreads();
   auto box_at = [&](int i) -> f32x4 { return i < LDS_BOXES ? s_box[i] : load_box(i); };
 
-  // ---- 3. chunked greedy sweep
+  // ---- 3. chunked greedy sweep.  With the sorted list in LDS (n <= NMS_SORT_LDS) the list is
+  // compacted after every chunk: the next chunk is always the 64 best boxes still alive, so the
+  // number of rounds follows the boxes that survive, not the candidate count.  Above that the chunk
+  // walks the sorted positions and skips suppressed ones by flag.
+  const bool compact = in_lds;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;  // 16 waves
-  for (int c0 = 0; c0 < m; c0 += 64) {
+  int m_cur = m;
+  for (int c0 = 0; c0 < m_cur;) {
     const int nk0 = s_nk;
     if (nk0 >= p.max_det) break;
     // (a) intra-chunk suppression masks: wave w tests columns c0+4w..c0+4w+3 against row c0+lane
+    const int i = c0 + lane;
+    const bool live = i < m_cur && !removed[i];
+    f32x4 bi = f32x4{0.f, 0.f, 0.f, 0.f};
     {
-      const int i = c0 + lane;
       unsigned bits = 0;
-      if (i < m && !removed[i]) {
-        const f32x4 bi = box_at(i);
+      if (live) {
+        bi = box_at(i);
         const float ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int j = c0 + 4 * wave + q;
-          if (j > i && j < m && !removed[j] && iou_gt(bi, ai, box_at(j), p.thr)) bits |= 1u << q;
+          if (j > i && j < m_cur && !removed[j] && iou_gt(bi, ai, box_at(j), p.thr)) bits |= 1u << q;
         }
       }
       cmask[lane][wave] = (unsigned char)bits;
     }
     __syncthreads();
-    // (b) wave 0 resolves the chunk: pure mask arithmetic on a wave-uniform live set
+    // (b) wave 0 resolves the chunk on scalar registers only (find-first-set, readlane of the kept
+    // row's mask, and-not), then every lane places itself by the rank of its bit in the kept mask
     if (wave == 0) {
-      const int i = c0 + lane;
       uint64_t rm = 0;
 #pragma unroll
       for (int w = 0; w < 16; ++w) rm |= (uint64_t)cmask[lane][w] << (4 * w);
-      const bool live = i < m && !removed[i];
-      uint64_t M = __ballot(live);
-      int nk = nk0, ck = 0;
+      uint64_t M = __ballot(live), K = 0;
+      int nk = nk0;
       while (M && nk < p.max_det) {
         const int t = __ffsll((long long)M) - 1;
         const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rm, t);
         const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(rm >> 32), t);
-        if (lane == t) {
-          kept_sorted[nk] = i;
-          chunk_box[ck] = box_at(i);
-        }
-        M &= ~(((uint64_t)hi << 32) | lo);
-        M &= ~(1ull << t);
-        ++nk; ++ck;
+        K |= 1ull << t;
+        M &= ~((((uint64_t)hi << 32) | lo) | (1ull << t));
+        ++nk;
+      }
+      if ((K >> lane) & 1) {
+        const int rank = __popcll(K & ((1ull << lane) - 1));
+        kept_slot[nk0 + rank] = order[i];
+        chunk_box[rank] = bi;
       }
       if (lane == 0) s_nk = nk;
     }
     __syncthreads();
     const int ck = s_nk - nk0;
     if (s_nk >= p.max_det) break;
-    // (c) suppress every later box against the chunk's kept boxes (all of which precede it)
-    for (int j = c0 + 64 + threadIdx.x; j < m; j += NMS_THREADS) {
-      if (removed[j]) continue;
-      const f32x4 bj = box_at(j);
-      for (int q = 0; q < ck; ++q) {
-        const f32x4 bq = chunk_box[q];
-        const float aq = (bq[2] - bq[0]) * (bq[3] - bq[1]);
-        if (iou_gt(bq, aq, bj, p.thr)) {
-          removed[j] = 1;
-          break;
+    // (c) suppress every later box against the chunk's kept boxes (all of which precede it).  The
+    // (box, kept box) pairs are spread over the whole workgroup: with R later boxes, G = 1024 / R
+    // thread groups (<= 16) each test every box against every G-th kept box; any hit sets the flag.
+    const int R = m_cur - (c0 + 64);
+    if (R > 0 && ck > 0) {
+      const int G = max(1, min(16, min(ck, NMS_THREADS / R)));
+      const int TS = NMS_THREADS / G;
+      const int grp = threadIdx.x / TS, r = threadIdx.x - grp * TS;
+      if (grp < G) {
+        for (int j = c0 + 64 + r; j < m_cur; j += TS) {
+          if (removed[j]) continue;
+          const f32x4 bj = box_at(j);
+          for (int q = grp; q < ck; q += G) {
+            const f32x4 bq = chunk_box[q];
+            const float aq = (bq[2] - bq[0]) * (bq[3] - bq[1]);
+            if (iou_gt(bq, aq, bj, p.thr)) {
+              removed[j] = 1;
+              break;
+            }
+          }
         }
       }
     }
+    __syncthreads();
+    if (!compact) {
+      c0 += 64;
+      continue;
+    }
+    // (d) compaction (c0 == 0): survivors of positions [64, m_cur) move to [0, R') in order.  Each
+    // thread owns a contiguous run of E <= 8 positions held in registers (all reads before the
+    // barrier, all writes after it); a wave scan + per-wave totals give the destinations.
+    if (R <= 0) break;
+    constexpr int EMAX = NMS_SORT_LDS / NMS_THREADS;
+    const int E = (R + NMS_THREADS - 1) / NMS_THREADS;
+    f32x4 kb[EMAX];
+    int ks[EMAX];
+    bool kv[EMAX];
+    int cnt = 0;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      const int pos = 64 + threadIdx.x * E + e;
+      kv[e] = e < E && pos < m_cur && !removed[pos];
+      if (kv[e]) {
+        kb[e] = box_at(pos);
+        ks[e] = order[pos];
+        ++cnt;
+      }
+    }
+    int incl = cnt;  // inclusive scan over the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    int off = incl - cnt, total = 0;
+#pragma unroll
+    for (int w = 0; w < NMS_THREADS / 64; ++w) {
+      const int t = s_wsum[w];
+      off += w < wave ? t : 0;
+      total += t;
+    }
+    int dst = off;
+#pragma unroll
+    for (int e = 0; e < EMAX; ++e) {
+      if (kv[e]) {
+        order[dst] = ks[e];
+        if (dst < LDS_BOXES) s_box[dst] = kb[e];
+        removed[dst] = 0;
+        ++dst;
+      }
+    }
+    m_cur = total;
     __syncthreads();
   }
   __syncthreads();
   const int kept = min(s_nk, p.max_det);
   for (int k = threadIdx.x; k < kept; k += NMS_THREADS) {
-    const int slot = order[kept_sorted[k]];
+    const int slot = kept_slot[k];
     const int64_t o = (int64_t)b * p.cap + slot;
     f32x4 v = *reinterpret_cast<const f32x4*>(p.cbox + o * 4);
     if (p.clip_w > 0.f) {
