@@ -224,6 +224,25 @@ def emit_stem2(m0: "Conv", m1: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int,
     return y
 
 
+def emit_merged(plan: Plan, convs, x: TV, out: TV, what="Conv1x1x2") -> TV:
+    """Several Convs that read the same x with the same kernel/stride/activation as ONE launch: the
+    folded weights/biases are concatenated along the output channels, in order, into `out`
+    (channel slices of one buffer), e.g. C3's cv2 and cv1 (U/nn/modules/block.py:259-273)."""
+    ws, bs = zip(*(m.folded() for m in convs))
+    c0 = convs[0].conv
+    k, st, pd, dl = c0.kernel_size[0], c0.stride[0], c0.padding[0], c0.dilation[0]
+    assert (out.h, out.w, out.c) == (*conv_out_hw(x.h, x.w, k, st, pd, dl), sum(w.shape[0] for w in ws))
+    emit_dense(plan, x, out, torch.cat(ws, 0), torch.cat(bs, 0), st, pd, dl, _act_code(convs[0].act), what=what)
+    return out
+
+
+def mergeable(convs) -> bool:
+    a = convs[0]
+    return all(type(m) is Conv and m.conv.kernel_size == a.conv.kernel_size and m.conv.stride == a.conv.stride
+               and m.conv.padding == a.conv.padding and m.conv.groups == 1 == a.conv.groups
+               and m.conv.dilation == a.conv.dilation and type(m.act) is type(a.act) for m in convs)
+
+
 def emit_seq(plan: Plan, mods, x, out=None):
     mods = list(mods)
     for i, m in enumerate(mods):
@@ -401,6 +420,12 @@ class C3(nn.Module):
 
     def emit(self, plan, x, out=None):
         c_ = self.cv1.conv.out_channels
+        if mergeable([self.cv2, self.cv1]) and not os.environ.get("YDBL_NO_MERGE"):
+            # cv2 and cv1 both read x: one launch into [m slot | cv2 | cv1] (cv3 reads the first 2c_)
+            buf = plan.alloc(x.n, x.h, x.w, 3 * c_)
+            emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
+            emit_seq(plan, self.m, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
+            return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
         buf = plan.alloc(x.n, x.h, x.w, 2 * c_)
         t = self.cv1.emit(plan, x)
         emit_seq(plan, self.m, t, buf.cslice(0, c_))
@@ -554,6 +579,11 @@ class C3AH(nn.Module):
 
     def emit(self, plan, x, out=None):
         c_ = self.cv1.conv.out_channels
+        if mergeable([self.cv2, self.cv1]) and not os.environ.get("YDBL_NO_MERGE"):
+            buf = plan.alloc(x.n, x.h, x.w, 3 * c_)  # [m slot | cv2 | cv1], as C3.emit
+            emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
+            self.m.emit(plan, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
+            return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
         buf = plan.alloc(x.n, x.h, x.w, 2 * c_)
         t = self.cv1.emit(plan, x)
         self.m.emit(plan, t, buf.cslice(0, c_))
