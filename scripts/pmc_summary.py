@@ -18,6 +18,8 @@ FAMILIES = {  # name keys, FETCH_SIZE multiplier
     "dsconv": (("dsconv_kernel",), 2),
     "stem": (("stem_kernel",), 2),
     "dwconv": (("dwconv_lds_kernel", "dwconv_kernel"), 2),
+    "bottleneck": (("bneck_kernel",), 2),
+    "stem2": (("stem2_kernel",), 2),
     "nms": (("nms_kernel",), 1),
 }
 
