@@ -150,6 +150,44 @@ def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
 
 
+@pytest.mark.parametrize("n,cin,cout,h,w,res", [
+    (2, 128, 64, 40, 40, "add"),      # 40-wide map: a half-empty last column tile
+    (3, 128, 64, 21, 19, "add"),      # ragged 8x16 tiles on both edges
+    (1, 128, 64, 17, 33, None),
+    (1, 128, 64, 5, 3, None),         # map smaller than one tile
+    (17, 64, 64, 40, 40, None),       # 64->64 is routed here for 25600 < N*H*W <= 65536
+    (30, 64, 64, 37, 29, "add"),
+])
+def test_conv3x3_vw(n, cin, cout, h, w, res):
+    """fp16 3x3 stride-1 128->64 and mid-size 64->64 convs: the VGPR-weight kernel (conv3x3.hip)."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    dtype = torch.float16
+    torch.manual_seed(cin * 3 + cout + h)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 1, 1))
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)  # channel slice of a wider buffer
+    ybuf = plan.alloc(n, h, w, cout + 8)
+    ybuf.torch().zero_()
+    yv = ybuf.cslice(8, cout)
+    rv, mode = None, _lib.RES_NONE
+    if res:
+        r = torch.randn(n, cout, h, w)
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD
+        ref = r.to(dtype).float() + ref
+    emit_dense(plan, xv, yv, wt, b, 1, 1, 1, _lib.ACT_SILU, rv, mode)
+    _run(plan)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
+    # the channels either side of the slice are untouched
+    full = ybuf.torch().float().cpu()
+    assert torch.count_nonzero(full[..., :8]) == 0 and torch.count_nonzero(full[..., 8 + cout:]) == 0
+
+
 @pytest.mark.parametrize("cin,cout,k,n,h,w,res", [
     (64, 64, 3, 2, 160, 160, "add"),  # halo-tiled kernel (>= 51200 px)
     (96, 40, 3, 2, 19, 23, None),     # block implicit GEMM, Cout tail

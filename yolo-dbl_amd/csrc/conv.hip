@@ -552,6 +552,9 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
 template <typename T, bool Q8>
 static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
   static const bool no_halo = getenv("YDBL_NO_HALO") != nullptr;  // A/B switch for scripts/conv_bench.py
+  if constexpr (sizeof(T) == 2 && !Q8) {
+    if (!no_halo && try_conv3x3_vw(a, kh, s)) return;
+  }
   if (!Q8 && try_tile<T>(a, kh, s)) return;
   if (!no_halo && try_conv3x3_halo<T, Q8>(a, kh, s)) return;
   if (try_wsk<T, Q8>(a, pw, s)) return;

@@ -188,6 +188,137 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   return true;
 }
 
+// ---- VGPR-weight 3x3 (fp16, stride 1, Cin 32..128): the bneck.hip layout for a single conv ----------
+// The halo kernel above reads both MFMA operands from LDS (a ds_read_b128 per 1.3 MFMAs) and walks Cin
+// in chunks behind two barriers each; on the head's 64/128-channel convs (Detect cv2, Bottleneck cv2)
+// that held it at 10-15 % of the MFMA rate, against ~30 % for the fused Bottleneck kernel.  Here, as
+// there: the whole (TH+2) x 18 input window with all Cin channels is staged once (one plane of 16-byte
+// records per 8-channel chunk, 1 KiB contiguous global reads per wave), one barrier, and each wave
+// keeps the A fragments of its TPW output-channel tiles in VGPRs for the whole launch, loaded straight
+// from the [Cout][KPAD] tap-major weight matrix (lane (co, g) at k-step m reads 8 consecutive input
+// channels of one tap: 16 contiguous bytes, no repacking).  Every B fragment read from LDS feeds TPW
+// MFMAs.  K order per 32-wide k-step: one tap x 4 chunks (lane group g = chunk 4i+g), so the lane
+// groups of a ds_read_b128 hit bank quads PIN*16 bytes apart (PIN a multiple of 16 records): conflict-free.
+// Fused epilogue (bias, act, residual, second output) from conv_common.hpp.
+template <int CIN, int TPW, int NWG, int TH, int ROWS>
+__global__ __launch_bounds__(256, 2) void conv3x3_vw_kernel(ConvArgs<_Float16> p, int tiles_x, int tiles_y, int ntiles,
+                                                            int co_splits) {
+  constexpr int CH = CIN / 8, KS = 9 * CH / 4, CPT = CH / 4;  // chunks, k-steps, k-steps per tap
+  constexpr int TW = 16, IP = TW + 2, IR = TH + 2, NPX = IR * IP, PIN = (NPX + 15) / 16 * 16;
+  constexpr int RW = 4 / NWG;  // waves sharing one output-channel group split the rows
+  static_assert(CH >= 4 && 32 % CH == 0 && TH % (RW * ROWS) == 0, "conv3x3_vw shape");
+  __shared__ __align__(16) unsigned char s_in[CH * PIN * 16];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  int t = xcd_remap(blockIdx.x, ntiles * co_splits);
+  const int cs = t % co_splits;  // output-channel slice of NWG * TPW * 16 channels
+  t /= co_splits;
+  const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y, img = t / (tiles_x * tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * TW;
+
+  // 1. input window rows oy0-1.., cols ox0-1..: item u*256 + tid -> chunk (tid >> 3) % CH,
+  // pixel px0 + u * PXU (8 consecutive pixels x CH chunks per wave instruction)
+  constexpr int PXU = 256 / CH, IT = (NPX + PXU - 1) / PXU;
+  const int s_chunk = (tid >> 3) % CH, px0 = ((tid >> 3) / CH) * 8 + (tid & 7);
+  h8 xr[IT];
+#pragma unroll
+  for (int u = 0; u < IT; ++u) {
+    const int px = px0 + u * PXU;
+    const int r = px / IP, c = px - r * IP;
+    const int iy = oy0 - 1 + r, ix = ox0 - 1 + c;
+    const bool ok = px < NPX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+    const _Float16* src = ok ? p.x + ((int64_t)(img * p.H + iy) * p.W + ix) * p.xcs + s_chunk * 8 : p.x;
+    const h8 v = *reinterpret_cast<const h8*>(src);
+    xr[u] = ok ? v : h8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  // this wave's A fragments: tiles cg*TPW .. +TPW-1 (16 output channels each)
+  const int cg = cs * NWG + wave % NWG;
+  h8 a[TPW][KS];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    const _Float16* wrow = p.w + (int64_t)((cg * TPW + tt) * 16 + r16) * p.KPAD + g * 8;
+#pragma unroll
+    for (int m = 0; m < KS; ++m)
+      a[tt][m] = *reinterpret_cast<const h8*>(wrow + (m / CPT) * CIN + (m % CPT) * 32);
+  }
+  unsigned char* s_dst = s_in + (s_chunk * PIN + px0) * 16;
+#pragma unroll
+  for (int u = 0; u < IT; ++u)
+    if (px0 + u * PXU < NPX) *reinterpret_cast<h8*>(s_dst + u * PXU * 16) = xr[u];
+  int co[TPW];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) co[tt] = (cg * TPW + tt) * 16 + 4 * g;
+  const unsigned char* in_b = s_in + (g * PIN + r16) * 16;
+  __syncthreads();
+
+  // 2. rows j0, j0+1 of the tile per pass; B for (row j, column r16, tap) at record (j+dy)*IP + r16+dx
+#pragma nounroll
+  for (int j0 = (wave / NWG) * ROWS; j0 < TH; j0 += RW * ROWS) {
+    f32x4 acc[TPW][ROWS];
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) acc[tt][r] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < KS; ++m) {
+      const int tap = m / CPT;
+      const int o = (((m % CPT) * 4) * PIN + (tap / 3) * IP + tap % 3) * 16;
+      h8 bf[ROWS];
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r) bf[r] = *reinterpret_cast<const h8*>(in_b + (j0 + r) * IP * 16 + o);
+#pragma unroll
+      for (int r = 0; r < ROWS; ++r)
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt)
+          acc[tt][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[tt][m], bf[r], acc[tt][r], 0, 0, 0);
+    }
+    int64_t pp[ROWS];
+    bool pv[ROWS];
+#pragma unroll
+    for (int r = 0; r < ROWS; ++r) {
+      const int oy = oy0 + j0 + r, ox = ox0 + r16;
+      pv[r] = oy < p.Ho && ox < p.Wo;
+      pp[r] = ((int64_t)img * p.Ho + oy) * p.Wo + ox;
+    }
+    conv_epilogue<_Float16, TPW, ROWS, false>(p, acc, pp, pv, co);
+  }
+}
+
+// TH16 > 0: 16-row tiles (ROWS16 rows per pass) when the map gives >= 1024 of them (half the halo
+// re-reads of 8-row tiles); only configurations that stay spill-free at 16 rows have one.
+template <int CIN, int TPW, int NWG, int ROWS8, int ROWS16 = 0>
+static void launch_vw(const ConvArgs<_Float16>& a, int cs, hipStream_t s) {
+  const int tiles_x = (int)cdiv(a.Wo, 16);
+  const int64_t t16 = (int64_t)a.N * cdiv(a.Ho, 16) * tiles_x;
+  if constexpr (ROWS16 > 0) {
+    if (t16 >= 1024) {
+      const int tiles_y = (int)cdiv(a.Ho, 16), nt = a.N * tiles_y * tiles_x;
+      conv3x3_vw_kernel<CIN, TPW, NWG, 16, ROWS16><<<(unsigned)(nt * cs), 256, 0, s>>>(a, tiles_x, tiles_y, nt, cs);
+      return;
+    }
+  }
+  const int tiles_y = (int)cdiv(a.Ho, 8), nt = a.N * tiles_y * tiles_x;
+  conv3x3_vw_kernel<CIN, TPW, NWG, 8, ROWS8><<<(unsigned)(nt * cs), 256, 0, s>>>(a, tiles_x, tiles_y, nt, cs);
+}
+
+// fp16 3x3 stride-1 pad-1 convs routed to the VGPR-weight kernel; false when the shape is not one of
+// them.  TPW output-channel tiles per wave, NWG wave groups over the channels (4 / NWG waves split the
+// rows): combinations that fit 256 VGPRs without scratch (scripts/kres.py).
+// Only the shapes where it measured faster than the halo / block-GEMM / tile kernels (conv_bench.py,
+// bs32, MI355X): 128->64 @40^2 32.3 -> 21.3 us, 64->64 @40^2 20.0 -> 16.5 us.  Every workgroup loads
+// all of its channels' weights into VGPRs, so on 80^2 maps (1600 workgroups) and for Cout 32/128 the
+// re-read loses (measured with the kernel open to Cin/Cout 32..128: 64->64 @80^2 41.7 -> 47.9,
+// 64->32 @80^2 22.5 -> 39.5, 64->128 @40^2 26.0 -> 29.4, 64->64 @20^2 8.9 -> 10.0 us).
+bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
+  static const bool off = getenv("YDBL_NO_VW") != nullptr;  // A/B switch for scripts/conv_bench.py
+  if (off || kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
+  if (a.xcs % 8 || a.H != a.Ho || a.W != a.Wo || (int64_t)a.N * a.Ho * a.Wo >= (1LL << 31)) return false;
+  if (a.Cin == 128 && a.Cout == 64) return launch_vw<128, 1, 4, 2>(a, 1, s), true;
+  if (a.Cin == 64 && a.Cout == 64 && a.P > 25600 && a.P <= 65536) return launch_vw<64, 2, 2, 4>(a, 1, s), true;
+  return false;
+}
+
 template bool try_conv3x3_halo<_Float16, false>(const ConvArgs<_Float16>&, int, hipStream_t);
 template bool try_conv3x3_halo<_Float16, true>(const ConvArgs<_Float16>&, int, hipStream_t);
 template bool try_conv3x3_halo<float, false>(const ConvArgs<float>&, int, hipStream_t);

@@ -67,6 +67,8 @@ __device__ __forceinline__ typename Op<T, Q8>::lds load_wop(const T* w, int64_t 
 // conv3x3.hip: halo-tiled 3x3 kernel for Cin >= 2 k-steps; false when the shape is not its own.
 template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s);
+// conv3x3.hip: fp16 3x3 stride-1 convs with Cin 32..128 and VGPR-resident weights.
+bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s);
 
 template <typename T>
 __device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a, const typename Vec<T>::type& b, f32x4 c);
