@@ -525,8 +525,12 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // maps whose Cout fits one 128-wide column (bigger pixel tiles re-read the weights less:
   // 512->128 1x1 @40^2 bs32 31.3 -> 23.0 us, 384->128 25.6 -> 19.4 us), 1024 otherwise
   // (128->192: 16.4 vs 21.4 us; DBL-s bs64 end to end 0.8 % faster at 1024).
+  // Shallow K (<= 128) on large maps: 2048 (8 per CU; each tile is a short k-loop, so more workgroups
+  // hide each other's load latency: 64->128 @80^2 bs32 35.3 -> 28.1 us, 64->64 17.5 -> 16.4,
+  // 128->64 22.2 -> 21.2).
   static const char* ov = getenv("YDBL_IGEMM_WANT");  // A/B knob for the benches
-  const int64_t want = ov && *ov ? atoi(ov) : (a.Cout <= 128 && a.P <= 65536 ? 512 : 1024);
+  const int64_t want = ov && *ov ? atoi(ov)
+                                 : (a.Cout <= 128 && a.P <= 65536 ? 512 : (a.K <= 128 && a.P > 65536 ? 2048 : 1024));
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   if (a.Cout <= 16) {
     if (blocks(256, 16) >= want) return launch_igemm<T, Q8, 256, 16, 4, 1>(a, pointwise, s);

@@ -228,7 +228,10 @@ static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, const float* 
 // double-buffered tile (more workgroups on the few pixels).
 template <typename T, int K, int S, int DIL>
 static int launch_ds(const ConvArgs<T>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
-  if (a.Wo > 20) launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, dwb, dw_act, s);
+  static const char* tv = getenv("YDBL_DS_TILE");  // A/B knob for scripts/ds_bench.py: 8 = 8x8 everywhere, S = 8x8 single-buffered
+  const char t = tv && *tv ? tv[0] : 'A';
+  if (t == 'S') launch_ds_tile<T, K, S, DIL, 8, 8, 2, false>(a, dww, dwb, dw_act, s);
+  else if (a.Wo > 20 && t != '8') launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, dwb, dw_act, s);
   else launch_ds_tile<T, K, S, DIL, 8, 8, 2, true>(a, dww, dwb, dw_act, s);
   return check_launch("ydbl_dsconv_nhwc");
 }
