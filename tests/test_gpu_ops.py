@@ -468,15 +468,17 @@ def test_dysample(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
-def test_lskblock(dtype):
+@pytest.mark.parametrize("c,h,w", [(64, 12, 10), (256, 20, 20), (512, 9, 13)])
+def test_lskblock(dtype, c, h, w):
+    """64 ch: per-thread 7x7 squeeze taps; 256/512 ch (DBL-n/s): taps split over 16 lanes + shuffles."""
     from oracle import model as om
     from ydbl.nn import modules as M
 
-    torch.manual_seed(4)
-    o = om.LSKblock(64).eval()
-    x = torch.randn(2, 64, 12, 10)
+    torch.manual_seed(4 + c)
+    o = om.LSKblock(c).eval()
+    x = torch.randn(2, c, h, w)
     tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
-    _module_parity(o, M.LSKblock(64), [x], dtype, tol)
+    _module_parity(o, M.LSKblock(c), [x], dtype, tol)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])

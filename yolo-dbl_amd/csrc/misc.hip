@@ -316,14 +316,19 @@ __global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<c
 }
 
 // ------------------------------------------------------------------ LSKblock gate
+// LSKA.py:46-52.  Stats: 32 lanes per pixel walk its channel vectors (coalesced 16-byte loads, 512 B
+// per pixel per wave instruction) and reduce sum / max over the 32 lanes; one launch of N*H*W*32
+// threads (a thread per pixel looping over all channels gave 50 workgroups at 20^2 bs32).
 template <typename T>
 __global__ __launch_bounds__(256) void lsk_stats_kernel(DView<const T> attn, float* __restrict__ agg) {
-  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (pix >= (int64_t)attn.n * attn.h * attn.w) return;
-  constexpr int V = Vec<T>::N;
-  const T* p = attn.pix(pix);
+  constexpr int V = Vec<T>::N, L = 32;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t pix = t / L;
+  const int sub = (int)(t % L);
+  const bool live = pix < (int64_t)attn.n * attn.h * attn.w;  // whole 32-lane groups share `live`
+  const T* p = attn.pix(live ? pix : 0);
   float s = 0.f, m = -INFINITY;
-  for (int c = 0; c < attn.c; c += V) {
+  for (int c = sub * V; c < attn.c; c += L * V) {
     float v[V];
     load_f<V>(p + c, v);
 #pragma unroll
@@ -332,10 +337,20 @@ __global__ __launch_bounds__(256) void lsk_stats_kernel(DView<const T> attn, flo
       m = fmaxf(m, v[q]);
     }
   }
-  agg[pix * 2 + 0] = s / float(attn.c);
-  agg[pix * 2 + 1] = m;
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) {
+    s += __shfl_xor(s, o);
+    m = fmaxf(m, __shfl_xor(m, o));
+  }
+  if (live && sub == 0) {
+    agg[pix * 2 + 0] = s / float(attn.c);
+    agg[pix * 2 + 1] = m;
+  }
 }
 
+// Gate: thread per (pixel, channel vector).  When a pixel's vectors fill whole 16-lane groups
+// (half % (16 V) == 0: every DBL config) the 2 x 49 taps of the 7x7 squeeze conv are split over
+// the 16 lanes and summed by xor-shuffles, instead of every thread redoing all 98.
 template <typename T>
 __global__ __launch_bounds__(256) void lsk_gate_kernel(DView<const T> attn, const float* __restrict__ agg,
                                                        const float* __restrict__ sw, const float* __restrict__ sb,
@@ -344,26 +359,31 @@ __global__ __launch_bounds__(256) void lsk_gate_kernel(DView<const T> attn, cons
   const int half = out.c;
   const int cg = half / V;
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)out.n * out.h * out.w * cg) return;
+  if (idx >= (int64_t)out.n * out.h * out.w * cg) return;  // 16-lane groups leave together (split path)
   const int c0 = (int)(idx % cg) * V;
   const int64_t pix = idx / cg;
   const int ox = (int)(pix % out.w);
   const int64_t t = pix / out.w;
   const int oy = (int)(t % out.h);
   const int b = (int)(t / out.h);
+  const bool split = cg % 16 == 0;  // uniform
+  const int t0 = split ? (int)(idx & 15) : 0, ts = split ? 16 : 1;
   float s0 = 0.f, s1 = 0.f;
-  for (int ci = 0; ci < 2; ++ci)
-    for (int ky = 0; ky < 7; ++ky) {
-      const int iy = oy - 3 + ky;
-      if (iy < 0 || iy >= out.h) continue;
-      for (int kx = 0; kx < 7; ++kx) {
-        const int ix = ox - 3 + kx;
-        if (ix < 0 || ix >= out.w) continue;
-        const float a = agg[(((int64_t)b * out.h + iy) * out.w + ix) * 2 + ci];
-        s0 = fmaf(sw[((0 * 2 + ci) * 7 + ky) * 7 + kx], a, s0);
-        s1 = fmaf(sw[((1 * 2 + ci) * 7 + ky) * 7 + kx], a, s1);
-      }
+  for (int tap = t0; tap < 98; tap += ts) {
+    const int ci = tap / 49, ky = (tap % 49) / 7, kx = tap % 7;
+    const int iy = oy - 3 + ky, ix = ox - 3 + kx;
+    if (iy < 0 || iy >= out.h || ix < 0 || ix >= out.w) continue;
+    const float a = agg[(((int64_t)b * out.h + iy) * out.w + ix) * 2 + ci];
+    s0 = fmaf(sw[((0 * 2 + ci) * 7 + ky) * 7 + kx], a, s0);
+    s1 = fmaf(sw[((1 * 2 + ci) * 7 + ky) * 7 + kx], a, s1);
+  }
+  if (split) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      s0 += __shfl_xor(s0, o);
+      s1 += __shfl_xor(s1, o);
     }
+  }
   s0 = sigmoidf_(s0 + sb[0]);
   s1 = sigmoidf_(s1 + sb[1]);
   float a1[V], a2[V], o[V];
@@ -515,11 +535,11 @@ extern "C" int ydbl_lsk_gate(const ydbl_view* attn, const float* sw, const float
   const int64_t npix = (int64_t)out->n * out->h * out->w;
   const int V = out->dtype == YDBL_F16 ? 8 : 4;
   if (out->dtype == YDBL_F16) {
-    lsk_stats_kernel<_Float16><<<nblk(npix), 256, 0, s>>>(cview<_Float16>(attn), agg);
+    lsk_stats_kernel<_Float16><<<nblk(npix * 32), 256, 0, s>>>(cview<_Float16>(attn), agg);
     lsk_gate_kernel<_Float16><<<nblk(npix * (out->c / V)), 256, 0, s>>>(cview<_Float16>(attn), agg, sw, sb,
                                                                          dview<_Float16>(*out));
   } else {
-    lsk_stats_kernel<float><<<nblk(npix), 256, 0, s>>>(cview<float>(attn), agg);
+    lsk_stats_kernel<float><<<nblk(npix * 32), 256, 0, s>>>(cview<float>(attn), agg);
     lsk_gate_kernel<float><<<nblk(npix * (out->c / V)), 256, 0, s>>>(cview<float>(attn), agg, sw, sb,
                                                                       dview<float>(*out));
   }
