@@ -24,6 +24,7 @@
  *   ydbl_dsconv_nhwc       <- DSConv.forward conv.py:91-108 (dw + pw + BN + SiLU, one kernel)
  *   ydbl_dwconv2d_nhwc     <- depthwise nn.Conv2d (DSConv.dw conv.py:98, DWConv conv.py:128-133,
  *                             GhostConv.cv2 conv.py:194, LSKblock.conv0/conv_spatial LSKA.py:31-32)
+ *   ydbl_dwconv2d_pair_nhwc<- LSKblock.forward LSKA.py:40-41 (conv0 -> conv_spatial, one launch)
  *   ydbl_letterbox         <- BasePredictor.preprocess engine/predictor.py:116-134 for ndarray frames:
  *                             LetterBox.__call__ data/augment.py:1535-1597 (cv2.resize INTER_LINEAR,
  *                             copyMakeBorder 114) + BGR->RGB + HWC->CHW + float /255
@@ -127,6 +128,11 @@ typedef struct {
   int32_t act, res_mode;
 } ydbl_dwconv_desc;
 int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream);
+
+/* Two chained depthwise convs, d1.x == d0.y: LSKblock's conv0 (5x5) -> conv_spatial (7x7, dil 3)
+ * (modules_attention/LSKA.py:40-41).  One launch with the whole map in LDS when H*W <= 512 (the P5
+ * maps at 640), bit-identical to the two ydbl_dwconv2d_nhwc launches it falls back to otherwise. */
+int ydbl_dwconv2d_pair_nhwc(const ydbl_dwconv_desc* d0, const ydbl_dwconv_desc* d1, void* stream);
 
 /* NCHW fp32 image batch -> NHWC view (channels >= 3 zero-filled up to y.cs), optional scale (1/255). */
 int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,

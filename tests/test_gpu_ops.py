@@ -468,9 +468,33 @@ def test_dysample(dtype):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
-@pytest.mark.parametrize("c,h,w", [(64, 12, 10), (256, 20, 20), (512, 9, 13)])
+@pytest.mark.parametrize("c,h,w", [(256, 20, 20), (64, 16, 32), (128, 7, 5)])
+def test_dw_pair_bit_identical(dtype, c, h, w):
+    """ydbl_dwconv2d_pair_nhwc (whole map in LDS) == the two ydbl_dwconv2d_nhwc launches, bit for bit."""
+    import torch.nn as nn
+
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(c + h)
+    c0 = nn.Conv2d(c, c, 5, padding=2, groups=c)
+    c1 = nn.Conv2d(c, c, 7, padding=9, groups=c, dilation=3)
+    x = torch.randn(3, c, h, w)
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x)
+    a1, a2 = M.emit_dw_pair(plan, c0, c1, xv)
+    b1 = M.emit_conv2d(plan, c0, xv, None)
+    b2 = M.emit_conv2d(plan, c1, b1, None)
+    _run(plan)
+    assert torch.equal(a1.torch(), b1.torch()) and torch.equal(a2.torch(), b2.torch())
+    ref1 = F.conv2d(x.to(dtype).float(), c0.weight.detach(), c0.bias.detach(), 1, 2, 1, c)
+    torch.testing.assert_close(a1.nchw().float().cpu(), ref1, **_tol(dtype))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("c,h,w", [(64, 12, 10), (256, 20, 20), (512, 9, 13), (64, 24, 24)])
 def test_lskblock(dtype, c, h, w):
-    """64 ch: per-thread 7x7 squeeze taps; 256/512 ch (DBL-n/s): taps split over 16 lanes + shuffles."""
+    """64 ch: per-thread 7x7 squeeze taps; 256/512 ch (DBL-n/s): taps split over 16 lanes + shuffles.
+    H*W <= 512: conv0 -> conv_spatial as one whole-map launch; 24x24: the two-launch fallback."""
     from oracle import model as om
     from ydbl.nn import modules as M
 

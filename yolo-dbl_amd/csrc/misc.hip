@@ -180,6 +180,104 @@ static bool launch_dw_lds(const ydbl_dwconv_desc* d, DView<const T> x, DView<T> 
   return false;
 }
 
+// ------------------------------------------------------------------ chained depthwise pair (LSK)
+// LSKA.py:40-41: a1 = conv0(x) (dw 5x5), a2 = conv_spatial(a1) (dw 7x7 dil 3).  On the small P5 maps
+// (20^2 at 640) the dilated 7x7 needs a 9-px halo, so an output tile drags in 3-6x its pixels and the
+// two launches cost 17 + 27 us (DBL-n bs32).  Here a workgroup owns one image x CV channel vectors
+// with the WHOLE map in LDS: x is staged once, a1 is computed into LDS (and stored, conv1 reads it),
+// a2 is computed from that.  Tap order (ky, kx) with padded taps skipped and fp32 FMAs as in
+// dwconv_lds_kernel, and a1 is rounded to T before phase 2 exactly as the two-launch path stores and
+// reloads it, so the outputs are bit-identical to it.
+constexpr int DWP_HWMAX = 512;
+// one phase: every thread owns channel vector cv of pixels pl, pl + LANES, ...  (Measured on DBL-n
+// bs32: this plain form, 36-38 us for both LSK depthwise convs, beat tap-unrolled variants with
+// 2-4 independent pixels in flight, 42-53 us: their LDS reads and code size cost more than the ILP
+// they bought.)
+template <typename T, int K, int D, int CV>
+__device__ __forceinline__ void dw_pair_phase(const typename Vec<T>::type* src, const f32x4* wts, const float* bias,
+                                              int pad, int act, DView<T> out, typename Vec<T>::type* keep, int b,
+                                              int cc, int cv, int pl, int H, int W) {
+  constexpr int V = Vec<T>::N, LANES = 256 / CV;
+  using vec = typename Vec<T>::type;
+  float bv[V];
+#pragma unroll
+  for (int q = 0; q < V; ++q) bv[q] = 0.f;
+  if (bias) load_f<V>(bias + cc, bv);
+  for (int p = pl; p < H * W; p += LANES) {
+    const int oy = p / W, ox = p % W;
+    float acc[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] = 0.f;
+#pragma unroll 1
+    for (int ky = 0; ky < K; ++ky) {
+      const int iy = oy - pad + ky * D;
+      if (iy < 0 || iy >= H) continue;
+#pragma unroll 1
+      for (int kx = 0; kx < K; ++kx) {
+        const int ix = ox - pad + kx * D;
+        if (ix < 0 || ix >= W) continue;  // padded taps contribute no term
+        const vec xv = src[(iy * W + ix) * CV + cv];
+#pragma unroll
+        for (int h = 0; h < V / 4; ++h) {
+          const f32x4 t4 = wts[((ky * K + kx) * CV + cv) * (V / 4) + h];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[4 * h + q] = fmaf(float(xv[4 * h + q]), t4[q], acc[4 * h + q]);
+        }
+      }
+    }
+    float o[V];
+#pragma unroll
+    for (int q = 0; q < V; ++q) o[q] = apply_act(bias ? acc[q] + bv[q] : acc[q], act);
+    store_f<V>(out.at(b, oy, ox) + cc, o);
+    if (keep) {
+      vec t;
+#pragma unroll
+      for (int q = 0; q < V; ++q) t[q] = (T)o[q];
+      keep[p * CV + cv] = t;
+    }
+  }
+}
+
+template <typename T, int K0, int D0, int K1, int D1, int CV>
+__global__ __launch_bounds__(256) void dw_pair_kernel(DView<const T> x, DView<T> y0, DView<T> y1,
+                                                      const float* __restrict__ w0, const float* __restrict__ b0,
+                                                      const float* __restrict__ w1, const float* __restrict__ b1,
+                                                      int pad0, int pad1, int act0, int act1) {
+  constexpr int V = Vec<T>::N;
+  using vec = typename Vec<T>::type;
+  __shared__ vec tx[DWP_HWMAX * CV], ta[DWP_HWMAX * CV];
+  __shared__ f32x4 ws0[K0 * K0 * CV * V / 4], ws1[K1 * K1 * CV * V / 4];
+  const int C = y0.c, H = x.h, W = x.w, HW = H * W;
+  const int cgroups = C / (CV * V);
+  const int b = blockIdx.x / cgroups, c0 = (blockIdx.x % cgroups) * CV * V;
+  {  // all of a thread's map loads in flight before the first LDS store
+    constexpr int IT = DWP_HWMAX * CV / 256;
+    vec tmp[IT];
+#pragma unroll
+    for (int u = 0; u < IT; ++u) {
+      const int i = threadIdx.x + u * 256, cv = i % CV, px = min(i / CV, HW - 1);
+      tmp[u] = vload(x.at(b, px / W, px % W) + c0 + cv * V);
+    }
+#pragma unroll
+    for (int u = 0; u < IT; ++u)
+      if (threadIdx.x + u * 256 < HW * CV) tx[threadIdx.x + u * 256] = tmp[u];
+  }
+  for (int i = threadIdx.x; i < K0 * K0 * CV * V / 4; i += 256) {
+    const int tap = i / (CV * V / 4), q = i % (CV * V / 4);
+    ws0[i] = *reinterpret_cast<const f32x4*>(w0 + tap * C + c0 + 4 * q);
+  }
+  for (int i = threadIdx.x; i < K1 * K1 * CV * V / 4; i += 256) {
+    const int tap = i / (CV * V / 4), q = i % (CV * V / 4);
+    ws1[i] = *reinterpret_cast<const f32x4*>(w1 + tap * C + c0 + 4 * q);
+  }
+  __syncthreads();
+  const int cv = threadIdx.x % CV, pl = threadIdx.x / CV;
+  const int cc = c0 + cv * V;
+  dw_pair_phase<T, K0, D0, CV>(tx, ws0, b0, pad0, act0, y0, ta, b, cc, cv, pl, H, W);
+  __syncthreads();
+  dw_pair_phase<T, K1, D1, CV>(ta, ws1, b1, pad1, act1, y1, nullptr, b, cc, cv, pl, H, W);
+}
+
 // ------------------------------------------------------------------ input NCHW fp32 -> NHWC
 template <typename T>
 __global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x, int n, int c, int h, int w,
@@ -221,18 +319,32 @@ __global__ __launch_bounds__(256) void gate_add_kernel(DView<const T> a, DView<c
 template <typename T>
 __global__ __launch_bounds__(256) void pool_up_concat_kernel(DView<const T> lo, DView<const T> mid,
                                                              DView<const T> hi, DView<T> y) {
+  // Work items are numbered segment by segment (all pool items, then all copies, then all
+  // upsamples), channel vector fastest: a wave takes one branch, instead of every wave (one output
+  // pixel = 64 vectors) running all three branches one after the other.
   constexpr int V = Vec<T>::N;
-  const int cg = y.c / V;
-  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (int64_t)y.n * y.h * y.w * cg) return;
-  int c = (int)(idx % cg) * V;
-  const int64_t pix = idx / cg;
+  const int clo = lo.p ? lo.c : 0, cmid = mid.p ? mid.c : 0;
+  const int64_t npix = (int64_t)y.n * y.h * y.w;
+  int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= npix * (y.c / V)) return;
+  int seg_c0 = 0, seg_cg = clo / V;
+  if (idx >= npix * seg_cg) {
+    idx -= npix * seg_cg;
+    seg_c0 = clo;
+    seg_cg = cmid / V;
+    if (idx >= npix * seg_cg) {
+      idx -= npix * seg_cg;
+      seg_c0 = clo + cmid;
+      seg_cg = (y.c - clo - cmid) / V;
+    }
+  }
+  const int c = seg_c0 + (int)(idx % seg_cg) * V;
+  const int64_t pix = idx / seg_cg;
   const int ox = (int)(pix % y.w);
   const int64_t t = pix / y.w;
   const int oy = (int)(t % y.h);
   const int b = (int)(t / y.h);
   float o[V];
-  const int clo = lo.p ? lo.c : 0, cmid = mid.p ? mid.c : 0;
   if (c < clo) {  // nn.AvgPool2d(2): mean of the 2x2 window (sum then / 4)
     float s[V], v[V];
     load_f<V>(lo.at(b, 2 * oy, 2 * ox) + c, s);
@@ -439,6 +551,37 @@ extern "C" int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream) {
                                                      cview<float>(res ? &d->r : nullptr), d->w, d->bias, d->kh, d->kw,
                                                      d->stride, d->pad, d->dil, d->act);
   return check_launch("ydbl_dwconv2d_nhwc");
+}
+
+extern "C" int ydbl_dwconv2d_pair_nhwc(const ydbl_dwconv_desc* d0, const ydbl_dwconv_desc* d1, void* stream) {
+  if (!d0 || !d1) return fail(YDBL_EINVAL, "dw_pair: null descriptor");
+  if (d1->x.ptr != d0->y.ptr || d1->x.cs != d0->y.cs || d1->x.c != d0->y.c)
+    return fail(YDBL_EINVAL, "dw_pair: d1.x must be d0.y");
+  const bool pair = d0->kh == 5 && d0->kw == 5 && d0->dil == 1 && d1->kh == 7 && d1->kw == 7 && d1->dil == 3 &&
+                    d0->stride == 1 && d1->stride == 1 && d0->res_mode == YDBL_RES_NONE &&
+                    d1->res_mode == YDBL_RES_NONE && d0->x.h == d0->y.h && d0->x.w == d0->y.w &&
+                    d1->y.h == d0->y.h && d1->y.w == d0->y.w && d0->x.h * d0->x.w <= DWP_HWMAX &&
+                    d0->x.dtype == d0->y.dtype && d1->y.dtype == d0->y.dtype && d0->x.c == d0->y.c &&
+                    d1->y.c == d0->y.c && d0->x.n == d0->y.n && d1->y.n == d0->y.n;
+  const int V = d0->x.dtype == YDBL_F16 ? 8 : 4;
+  constexpr int CV = 2;  // 16 (f16) / 8 (f32) channels per workgroup (CV = 1: 42 vs 38 us)
+  if (!pair || d0->y.c % (CV * V) || !d0->w || !d1->w || check_view(&d0->x, "dw_pair.x", true) ||
+      check_view(&d0->y, "dw_pair.y0", true) || check_view(&d1->y, "dw_pair.y1", true)) {
+    // not the fused geometry: the two launches
+    const int r = ydbl_dwconv2d_nhwc(d0, stream);
+    return r ? r : ydbl_dwconv2d_nhwc(d1, stream);
+  }
+  hipStream_t s = as_stream(stream);
+  const unsigned blocks = (unsigned)(d0->y.n * (d0->y.c / (CV * V)));
+  if (d0->x.dtype == YDBL_F16)
+    dw_pair_kernel<_Float16, 5, 1, 7, 3, CV><<<blocks, 256, 0, s>>>(
+        cview<_Float16>(&d0->x), dview<_Float16>(d0->y), dview<_Float16>(d1->y), d0->w, d0->bias, d1->w, d1->bias,
+        d0->pad, d1->pad, d0->act, d1->act);
+  else
+    dw_pair_kernel<float, 5, 1, 7, 3, CV><<<blocks, 256, 0, s>>>(
+        cview<float>(&d0->x), dview<float>(d0->y), dview<float>(d1->y), d0->w, d0->bias, d1->w, d1->bias, d0->pad,
+        d1->pad, d0->act, d1->act);
+  return check_launch("ydbl_dwconv2d_pair_nhwc");
 }
 
 extern "C" int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,

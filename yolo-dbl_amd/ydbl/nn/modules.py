@@ -89,9 +89,9 @@ def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None
         plan.fp8_candidates.append((d, x, wk32))  # see ydbl.quant: e4m3 operands after calibration
 
 
-def emit_dw(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,
-            act=_lib.ACT_NONE, res: TV | None = None, what="dwconv"):
-    """Depthwise conv; w fp32 [c, 1, kh, kw]."""
+def dw_desc(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,
+            act=_lib.ACT_NONE, res: TV | None = None):
+    """Depthwise conv descriptor (+ the device constants it points at); w fp32 [c, 1, kh, kw]."""
     c, _, kh, kw = w.shape
     assert c == x.c == y.c
     wd = plan.const(w.float().reshape(c, kh * kw).t().contiguous())
@@ -99,7 +99,33 @@ def emit_dw(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, s
     d = DwConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(), wd.data_ptr(),
                    bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, act,
                    _lib.RES_ADD if res is not None else _lib.RES_NONE)
-    plan.launch("ydbl_dwconv2d_nhwc", d, what=what, keep=[wd, bd, d])
+    return d, [wd, bd, d]
+
+
+def emit_dw(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,
+            act=_lib.ACT_NONE, res: TV | None = None, what="dwconv"):
+    """Depthwise conv; w fp32 [c, 1, kh, kw]."""
+    d, keep = dw_desc(plan, x, y, w, b, stride, pad, dil, act, res)
+    plan.launch("ydbl_dwconv2d_nhwc", d, what=what, keep=keep)
+
+
+def emit_dw_pair(plan: Plan, c0: nn.Conv2d, c1: nn.Conv2d, x: TV, what="dw_pair") -> tuple[TV, TV]:
+    """Two chained depthwise nn.Conv2d (c1 reads c0's output) as one ydbl_dwconv2d_pair_nhwc launch
+    (the library falls back to two launches for geometries it does not fuse)."""
+    descs, keep = [], []
+    src, outs = x, []
+    for conv in (c0, c1):
+        k, s, p, d = conv.kernel_size[0], conv.stride[0], conv.padding[0], conv.dilation[0]
+        ho, wo = conv_out_hw(src.h, src.w, k, s, p, d)
+        y = plan.alloc(src.n, ho, wo, conv.out_channels)
+        b = conv.bias.detach().float().cpu() if conv.bias is not None else None
+        dd, kk = dw_desc(plan, src, y, conv.weight.detach().float().cpu(), b, s, p, d)
+        descs.append(dd)
+        keep += kk
+        outs.append(y)
+        src = y
+    plan.launch("ydbl_dwconv2d_pair_nhwc", descs[0], descs[1], what=what, keep=keep)
+    return outs[0], outs[1]
 
 
 def conv_out_hw(h, w, k, s, p, d):
@@ -728,8 +754,7 @@ class LSKblock(nn.Module):
 
     def emit(self, plan, x, out=None):
         half = self.conv1.out_channels
-        a1 = emit_conv2d(plan, self.conv0, x, None, what="LSK.dw5")
-        a2 = emit_conv2d(plan, self.conv_spatial, a1, None, what="LSK.dw7d3")
+        a1, a2 = emit_dw_pair(plan, self.conv0, self.conv_spatial, x, what="LSK.dw5+dw7d3")
         attn = plan.alloc(x.n, x.h, x.w, 2 * half)
         emit_conv2d(plan, self.conv1, a1, attn.cslice(0, half), what="LSK.conv1")
         emit_conv2d(plan, self.conv2, a2, attn.cslice(half, half), what="LSK.conv2")
