@@ -118,13 +118,14 @@ def test_conv_tile(dtype, cin, cout, s, h, w, res):
 @pytest.mark.parametrize("n,cin,cout,h,w,res", [
     (2, 64, 32, 161, 163, None),      # ragged 8x16 tiles on both edges, Cout 32 (NTN 2)
     (2, 128, 64, 160, 160, "add"),    # residual add (Bottleneck), one 64-channel split
-    (1, 64, 128, 200, 256, None),     # 4-row tiles (few workgroups), two output-channel splits
-    (2, 256, 48, 170, 152, "add"),    # 4-row tiles, Cout not a multiple of 16
+    (1, 64, 128, 200, 256, None),     # two output-channel splits
+    (2, 256, 48, 170, 152, "add"),    # Cout not a multiple of 16
+    (32, 384, 64, 40, 40, None),      # DBL-n head Bottleneck cv1 (deep Cin, 40-wide map: ragged column tile)
     (2, 64, 96, 256, 256, None),      # 16-row tiles, partial second output-channel split
     (2, 320, 80, 160, 176, "add"),    # deep Cin (> 256) on a map large enough for the halo path
 ])
 def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
-    """3x3 stride-1 convs with Cin >= 64 on >= 51200 output pixels: the halo-tiled kernel (4/8/16-row tiles)."""
+    """3x3 stride-1 convs with Cin >= 64 on >= 51200 output pixels: the halo-tiled kernel (8/16-row tiles)."""
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense
 

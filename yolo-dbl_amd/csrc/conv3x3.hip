@@ -167,8 +167,7 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
 // 3x3, pad 1, dil 1, stride 1/2, Cin a multiple of BK and >= 2 chunks.  Returns false when the
 // shape is not this kernel's (the caller falls back to the implicit-GEMM kernels).
 // Where the halo tile beats the implicit GEMM (scripts/conv_bench.py, fp16, MI355X): stride 1 on
-// >= 51200 output pixels, except deep-K convs with few output columns (384->64 @40^2 bs32 stays
-// on conv_wsk_kernel, 79 vs 86 us).  Measured: 256->32 @80^2 bs32 132 -> 62 us, 512->64 @80^2 bs64
+// >= 51200 output pixels.  Measured: 256->32 @80^2 bs32 132 -> 62 us, 512->64 @80^2 bs64
 // 714 -> 382 us, 768->128 @40^2 bs64 534 -> 348 us, 1024->128 @160^2 bs8 1371 -> 688 us.
 // 16-row tiles where the map allows (weights staged once per 256 pixels instead of 128),
 // 4-row tiles when 8-row tiles would leave fewer than 512 workgroups.
@@ -177,13 +176,21 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   constexpr int BK = 4 * Vec<T>::N;
   if (kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
   if (a.Cin % BK || a.Cin < 2 * BK || a.xcs % Vec<T>::N) return false;
+  static const char* fth = getenv("YDBL_HALO_TH");  // A/B knob for scripts/conv_bench.py: force 4/8/16-row tiles
+  const int force_th = fth && *fth ? atoi(fth) : 0;
   if ((int64_t)a.P < 51200) return false;
-  if (a.Cin > 256 && (int64_t)a.P * a.Cout <= 51200LL * 64) return false;
+  if (force_th == 4) return launch_halo<T, Q8, 1, 4>(a, s), true;
+  if (force_th == 8) return launch_halo<T, Q8, 1, 8>(a, s), true;
+  if (force_th == 16) return launch_halo<T, Q8, 1, 16>(a, s), true;
   const int64_t csplit = cdiv(a.Cout, 64);
   const int64_t tiles8 = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * csplit;
   const int64_t tiles16 = (int64_t)a.N * cdiv(a.Ho, 16) * cdiv(a.Wo, 16) * csplit;
+  // No 4-row tiles by default: every workgroup re-reads all of its channels' weights, so at 480
+  // 8-row tiles (40^2 bs32, Cout 64) the doubled grid lost (YDBL_HALO_TH A/B: 384->64 88.9 vs
+  // 49.6 us, 192->64 45.9 vs 28.0 us); 384->64 @40^2 also beats the wave-split-K kernel it used to
+  // take (78.8 us).  (P >= 51200 already guarantees >= 400 8-row tiles.)
+  (void)tiles8;
   if (a.Ho % 16 == 0 && a.Cout > 32 && tiles16 >= 512) launch_halo<T, Q8, 1, 16>(a, s);
-  else if (tiles8 < 512) launch_halo<T, Q8, 1, 4>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);
   return true;
 }
