@@ -403,26 +403,25 @@ __global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<c
   const float wsw = (float(x1) - ix) * (iy - float(y0));
   const float wse = (ix - float(x0)) * (iy - float(y0));
   const int c0 = gi * cpg + cv * V;
-  float acc[V], v[V];
+  // The four corner loads are unconditional (clamped addresses, the out-of-range corner's weight
+  // zeroed: acc + v * 0 = acc exactly, v finite), so they are in flight together instead of each
+  // behind its own branch and wait.  Terms are added in grid_sample's nw, ne, sw, se order.
+  const bool xin = x1 < W, yin = y1 < H;
+  const int x1c = xin ? x1 : x0, y1c = yin ? y1 : y0;
+  float vnw[V], vne[V], vsw[V], vse[V];
+  load_f<V>(x.at(b, y0, x0) + c0, vnw);
+  load_f<V>(x.at(b, y0, x1c) + c0, vne);
+  load_f<V>(x.at(b, y1c, x0) + c0, vsw);
+  load_f<V>(x.at(b, y1c, x1c) + c0, vse);
+  const float kne = xin ? wne : 0.f, ksw = yin ? wsw : 0.f, kse = xin && yin ? wse : 0.f;
+  float acc[V];
 #pragma unroll
-  for (int q = 0; q < V; ++q) acc[q] = 0.f;
-  load_f<V>(x.at(b, y0, x0) + c0, v);
-#pragma unroll
-  for (int q = 0; q < V; ++q) acc[q] += v[q] * wnw;
-  if (x1 < W) {
-    load_f<V>(x.at(b, y0, x1) + c0, v);
-#pragma unroll
-    for (int q = 0; q < V; ++q) acc[q] += v[q] * wne;
-  }
-  if (y1 < H) {
-    load_f<V>(x.at(b, y1, x0) + c0, v);
-#pragma unroll
-    for (int q = 0; q < V; ++q) acc[q] += v[q] * wsw;
-  }
-  if (x1 < W && y1 < H) {
-    load_f<V>(x.at(b, y1, x1) + c0, v);
-#pragma unroll
-    for (int q = 0; q < V; ++q) acc[q] += v[q] * wse;
+  for (int q = 0; q < V; ++q) {
+    acc[q] = 0.f;
+    acc[q] += vnw[q] * wnw;
+    acc[q] += vne[q] * kne;
+    acc[q] += vsw[q] * ksw;
+    acc[q] += vse[q] * kse;
   }
   store_f<V>(y.at(b, oy2, ox2) + c0, acc);
 }
