@@ -217,8 +217,15 @@ static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, const float* 
     const int cs = (int)cdiv(a.Cout, ntn * 16);
     kern<<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y, cs);
   };
+  static const char* fn = getenv("YDBL_DS_NTN");  // A/B knob for scripts/ds_bench.py: force 2/4 output tiles
+  const int force = fn && *fn ? atoi(fn) : 0;
+  if (force == 2) return go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
+  if (force == 4) return go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
   if (a.Cout <= 32) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
-  else if (a.Cout <= 64 || ntiles < 256) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
+  // k3 s1 with < 512 tiles: two 64-channel column workgroups per tile (the cheap depthwise phase is
+  // recomputed; 128->128 @20^2 bs32 15.0 -> 11.8 us; k7 loses: 19.7 -> 25.4)
+  else if (a.Cout <= 64 || ntiles < 256 || (K == 3 && S == 1 && ntiles < 512))
+    go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
   else go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 8, DBUF>, 8);
 }
 
