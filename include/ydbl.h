@@ -271,9 +271,16 @@ typedef struct {
   int32_t add;
   int32_t tile_h;
   const void* params;
+  int32_t c_mid;     /* intermediate channels: 0 = c/2 (Bottleneck e=0.5); 64 with c = 64 (Detect box branch) */
 } ydbl_bottleneck_desc;
 int64_t ydbl_bottleneck_params_size(int32_t c);
 int ydbl_bottleneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c, void* out);
+/* Same kernel for any (c, c_mid) pair it is built for -- (16,8) (32,16) (64,32) (64,64): two chained
+ * 3x3 stride-1 Conv+SiLU, c -> c_mid -> c.  (64,64) replaces the Detect head's box-branch
+ * cv2[i][0] -> cv2[i][1] (nn/modules/head.py:86-90) at 64 channels. */
+int64_t ydbl_conv3x3_pair_params_size(int32_t c, int32_t c_mid);
+int ydbl_conv3x3_pair_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c,
+                           int32_t c_mid, void* out);
 int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream);
 
 /* LetterBox a batch of HWC uint8 BGR frames into one fp32 NCHW RGB canvas batch (values /255).

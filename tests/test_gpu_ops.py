@@ -389,18 +389,21 @@ def test_stem2(c0, n, h, w):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("c,n,h,w,add,tile_h,cs_extra", [
-    (16, 2, 64, 64, True, 0, 0), (32, 1, 37, 53, True, 0, 8), (64, 2, 80, 80, True, 0, 0),
-    (64, 1, 17, 100, False, 8, 0), (16, 3, 5, 3, True, 16, 8), (32, 2, 40, 48, False, 16, 0),
-    (64, 3, 48, 33, True, 16, 16), (16, 1, 1, 1, True, 8, 0), (64, 8, 80, 80, True, 8, 0)])
-def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra):
-    """ydbl_bottleneck_nhwc (cv1 3x3 c->c/2, cv2 3x3 c/2->c, SiLU, optional x + ..., fp16) vs the two
+@pytest.mark.parametrize("c,n,h,w,add,tile_h,cs_extra,cm", [
+    (16, 2, 64, 64, True, 0, 0, 0), (32, 1, 37, 53, True, 0, 8, 0), (64, 2, 80, 80, True, 0, 0, 0),
+    (64, 1, 17, 100, False, 8, 0, 0), (16, 3, 5, 3, True, 16, 8, 0), (32, 2, 40, 48, False, 16, 0, 0),
+    (64, 3, 48, 33, True, 16, 16, 0), (16, 1, 1, 1, True, 8, 0, 0), (64, 8, 80, 80, True, 8, 0, 0),
+    # c_mid = 64: the Detect box branch Conv(64,64,3) -> Conv(64,64,3) (head.py:86-90)
+    (64, 2, 80, 80, False, 0, 0, 64), (64, 3, 37, 29, False, 8, 8, 64), (64, 1, 5, 3, True, 0, 0, 64)])
+def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra, cm):
+    """ydbl_bottleneck_nhwc (cv1 3x3 c->c_mid, cv2 3x3 c_mid->c, SiLU, optional x + ..., fp16) vs the two
     convs in fp32 on fp16-rounded operands, the intermediate rounded to fp16 as the unfused path stores it
     (U/nn/modules/block.py:355-357)."""
     from ydbl import _lib
 
-    torch.manual_seed(c * 7 + h)
-    cm = c // 2
+    torch.manual_seed(c * 7 + h + cm)
+    cmid = cm
+    cm = cm or c // 2
     x = torch.randn(n, c, h, w)
     w1 = torch.randn(cm, c, 3, 3) / (9 * c) ** 0.5
     b1 = torch.randn(cm) * 0.5
@@ -414,11 +417,16 @@ def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra):
     plan = _plan(torch.float16)
     xv = _tv_from_nchw(plan, x, cs_extra=cs_extra)
     yv = plan.alloc(n, h, w, c, cs=c + cs_extra)  # channel stride wider than c (concat slice)
-    host = torch.empty(int(_lib.lib.ydbl_bottleneck_params_size(c)), dtype=torch.uint8)
-    _lib.check(_lib.lib.ydbl_bottleneck_pack(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), c,
-                                             host.data_ptr()))
+    if cmid:
+        host = torch.empty(int(_lib.lib.ydbl_conv3x3_pair_params_size(c, cm)), dtype=torch.uint8)
+        _lib.check(_lib.lib.ydbl_conv3x3_pair_pack(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), c,
+                                                   cm, host.data_ptr()))
+    else:
+        host = torch.empty(int(_lib.lib.ydbl_bottleneck_params_size(c)), dtype=torch.uint8)
+        _lib.check(_lib.lib.ydbl_bottleneck_pack(w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), c,
+                                                 host.data_ptr()))
     params = host.to(DEV)
-    d = _lib.BottleneckDesc(xv.struct(), yv.struct(), c, int(add), tile_h, params.data_ptr())
+    d = _lib.BottleneckDesc(xv.struct(), yv.struct(), c, int(add), tile_h, params.data_ptr(), cmid)
     plan.launch("ydbl_bottleneck_nhwc", d)
     _run(plan)
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, rtol=1e-2, atol=1e-2)
@@ -437,6 +445,10 @@ def test_bottleneck_rejects_bad_shapes():
         d = _lib.BottleneckDesc(xv.struct(), yv.struct(), c, 1, tile_h, params.data_ptr())
         assert _lib.lib.ydbl_bottleneck_nhwc(ctypes.byref(d), None) != 0
     assert _lib.lib.ydbl_bottleneck_params_size(48) == -1
+    assert _lib.lib.ydbl_conv3x3_pair_params_size(32, 32) == -1
+    xv, yv = plan.alloc(1, 16, 16, 64), plan.alloc(1, 16, 16, 64)
+    d = _lib.BottleneckDesc(xv.struct(), yv.struct(), 64, 0, 16, params.data_ptr(), 64)  # c_mid 64: 8-row only
+    assert _lib.lib.ydbl_bottleneck_nhwc(ctypes.byref(d), None) != 0
 
 
 def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False):

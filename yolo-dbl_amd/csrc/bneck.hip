@@ -55,9 +55,9 @@ constexpr int ksteps() {
 }
 constexpr int rup16(int v) { return (v + 15) / 16 * 16; }
 
-template <int C, int TH>
+template <int C, int CMID, int TH>
 struct BneckCfg {
-  static constexpr int CM = C / 2, CH = C / 8, CHM = (CM + 7) / 8;
+  static constexpr int CM = CMID, CH = C / 8, CHM = (CM + 7) / 8;
   static constexpr int NT1 = (CM + 15) / 16, NT2 = C / 16;
   static constexpr int KS1 = ksteps<CH>(), KS2 = ksteps<CHM>();
   static constexpr int TW = 16;
@@ -79,9 +79,9 @@ struct BneckCfg {
 
 // Host: fp32 PyTorch-layout weights (BN folded) -> fragment blob.  A[row][k]: row = output channel of
 // the 16-channel tile, k = 32m + 8g + j -> (kslot(m, g), channel chunk*8 + j).
-template <int C>
+template <int C, int CMID>
 void bneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, unsigned char* out) {
-  using Cfg = BneckCfg<C, 16>;
+  using Cfg = BneckCfg<C, CMID, 16>;
   constexpr int CM = Cfg::CM;
   _Float16* f1 = reinterpret_cast<_Float16*>(out);
   _Float16* f2 = f1 + Cfg::W1F * 8;
@@ -121,11 +121,11 @@ __device__ __forceinline__ int kbase(int g) {
   return CH >= 4 ? g * PL * 16 : 0;
 }
 
-template <int C, int TH, bool ADD>
+template <int C, int CMID, int TH, bool ADD>
 __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, DView<_Float16> y,
                                                        const unsigned char* __restrict__ params, int tiles_x,
                                                        int tiles_y, int ntiles) {
-  using Cfg = BneckCfg<C, TH>;
+  using Cfg = BneckCfg<C, CMID, TH>;
   constexpr int CH = Cfg::CH, CHM = Cfg::CHM, CM = Cfg::CM;
   constexpr int IP = Cfg::IP, MP = Cfg::MP, PIN = Cfg::PIN, PMID = Cfg::PMID;
   constexpr int NT1 = Cfg::NT1, NT2 = Cfg::NT2, KS1 = Cfg::KS1, KS2 = Cfg::KS2;
@@ -264,26 +264,38 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
 
 using namespace ydbl;
 
-extern "C" int64_t ydbl_bottleneck_params_size(int32_t c) {
-  if (c == 16) return BneckCfg<16, 16>::BYTES;
-  if (c == 32) return BneckCfg<32, 16>::BYTES;
-  if (c == 64) return BneckCfg<64, 16>::BYTES;
+// (c, c_mid) pairs built: the backbone Bottleneck(c, c, e=0.5) chains and the Detect head's box
+// branch cv2[i][0:2] = Conv(64, 64, 3) -> Conv(64, 64, 3) (head.py:86-90, no shortcut).
+static int64_t pair_bytes(int c, int cm) {
+  if (c == 16 && cm == 8) return BneckCfg<16, 8, 16>::BYTES;
+  if (c == 32 && cm == 16) return BneckCfg<32, 16, 16>::BYTES;
+  if (c == 64 && cm == 32) return BneckCfg<64, 32, 16>::BYTES;
+  if (c == 64 && cm == 64) return BneckCfg<64, 64, 16>::BYTES;
   return -1;
+}
+
+extern "C" int64_t ydbl_bottleneck_params_size(int32_t c) { return pair_bytes(c, c / 2); }
+extern "C" int64_t ydbl_conv3x3_pair_params_size(int32_t c, int32_t c_mid) { return pair_bytes(c, c_mid); }
+
+extern "C" int ydbl_conv3x3_pair_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c,
+                                      int32_t c_mid, void* out) {
+  if (!w1 || !b1 || !w2 || !b2 || !out) return fail(YDBL_EINVAL, "bottleneck_pack: null pointer");
+  auto* o = reinterpret_cast<unsigned char*>(out);
+  if (c == 16 && c_mid == 8) { bneck_pack<16, 8>(w1, b1, w2, b2, o); return 0; }
+  if (c == 32 && c_mid == 16) { bneck_pack<32, 16>(w1, b1, w2, b2, o); return 0; }
+  if (c == 64 && c_mid == 32) { bneck_pack<64, 32>(w1, b1, w2, b2, o); return 0; }
+  if (c == 64 && c_mid == 64) { bneck_pack<64, 64>(w1, b1, w2, b2, o); return 0; }
+  return fail(YDBL_EINVAL, "bottleneck_pack: (c, c_mid) must be (16, 8), (32, 16), (64, 32) or (64, 64)");
 }
 
 extern "C" int ydbl_bottleneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c,
                                     void* out) {
-  if (!w1 || !b1 || !w2 || !b2 || !out) return fail(YDBL_EINVAL, "bottleneck_pack: null pointer");
-  auto* o = reinterpret_cast<unsigned char*>(out);
-  if (c == 16) { bneck_pack<16>(w1, b1, w2, b2, o); return 0; }
-  if (c == 32) { bneck_pack<32>(w1, b1, w2, b2, o); return 0; }
-  if (c == 64) { bneck_pack<64>(w1, b1, w2, b2, o); return 0; }
-  return fail(YDBL_EINVAL, "bottleneck_pack: c must be 16, 32 or 64");
+  return ydbl_conv3x3_pair_pack(w1, b1, w2, b2, c, c / 2, out);
 }
 
-template <int C, int TH>
+template <int C, int CMID, int TH>
 static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
-  using Cfg = BneckCfg<C, TH>;
+  using Cfg = BneckCfg<C, CMID, TH>;
   const int tiles_x = (int)cdiv(d->y.w, Cfg::TW), tiles_y = (int)cdiv(d->y.h, TH);
   const int64_t nt = (int64_t)tiles_x * tiles_y * d->y.n;
   if (nt > 0x7fffffff) return fail(YDBL_EINVAL, "bottleneck: grid too large");
@@ -291,18 +303,19 @@ static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
   auto y = dview<_Float16>(d->y);
   auto* p = reinterpret_cast<const unsigned char*>(d->params);
   if (d->add)
-    bneck_kernel<C, TH, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
+    bneck_kernel<C, CMID, TH, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
   else
-    bneck_kernel<C, TH, false><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
+    bneck_kernel<C, CMID, TH, false><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
   return check_launch("ydbl_bottleneck_nhwc");
 }
 
-template <int C>
+template <int C, int CMID>
 static int bneck_dispatch(const ydbl_bottleneck_desc* d, hipStream_t s) {
   // 16-row tiles halve the halo recompute; 8-row tiles when 16-row ones leave the chip under-filled
+  // (and always for c_mid = 64: its 16-row tile would need 102 KB of LDS, one workgroup per CU)
   const int64_t t16 = cdiv(d->y.h, 16) * cdiv(d->y.w, 16) * (int64_t)d->y.n;
-  const int th = d->tile_h ? d->tile_h : (t16 >= 1024 ? 16 : 8);
-  return th == 16 ? bneck_go<C, 16>(d, s) : bneck_go<C, 8>(d, s);
+  const int th = d->tile_h ? d->tile_h : (t16 >= 1024 && CMID < 64 ? 16 : 8);
+  return th == 16 ? bneck_go<C, CMID, 16>(d, s) : bneck_go<C, CMID, 8>(d, s);
 }
 
 extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream) {
@@ -310,7 +323,7 @@ extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream)
   if (!d->params) return fail(YDBL_EINVAL, "bottleneck: null parameters");
   if (check_view(&d->x, "bottleneck.x", true) || check_view(&d->y, "bottleneck.y", true)) return YDBL_EINVAL;
   if (d->x.dtype != YDBL_F16 || d->y.dtype != YDBL_F16) return fail(YDBL_EINVAL, "bottleneck: fp16 views only");
-  const int c = d->c;
+  const int c = d->c, cm = d->c_mid ? d->c_mid : d->c / 2;
   if (d->x.c != c || d->y.c != c) return fail(YDBL_EINVAL, "bottleneck: x.c and y.c must equal c");
   if (d->x.n != d->y.n || d->x.h != d->y.h || d->x.w != d->y.w)
     return fail(YDBL_EINVAL, "bottleneck: x and y shapes differ");
@@ -318,8 +331,12 @@ extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream)
   if (d->tile_h != 0 && d->tile_h != 8 && d->tile_h != 16) return fail(YDBL_EINVAL, "bottleneck: tile_h must be 0, 8 or 16");
   if (d->x.ptr == d->y.ptr) return fail(YDBL_EINVAL, "bottleneck: in-place is not supported (halo reads)");
   hipStream_t s = as_stream(stream);
-  if (c == 16) return bneck_dispatch<16>(d, s);
-  if (c == 32) return bneck_dispatch<32>(d, s);
-  if (c == 64) return bneck_dispatch<64>(d, s);
-  return fail(YDBL_EINVAL, "bottleneck: c must be 16, 32 or 64");
+  if (c == 16 && cm == 8) return bneck_dispatch<16, 8>(d, s);
+  if (c == 32 && cm == 16) return bneck_dispatch<32, 16>(d, s);
+  if (c == 64 && cm == 32) return bneck_dispatch<64, 32>(d, s);
+  if (c == 64 && cm == 64) {
+    if (d->tile_h == 16) return fail(YDBL_EINVAL, "bottleneck: c_mid 64 takes 8-row tiles only");
+    return bneck_go<64, 64, 8>(d, s);
+  }
+  return fail(YDBL_EINVAL, "bottleneck: (c, c_mid) must be (16, 8), (32, 16), (64, 32) or (64, 64)");
 }

@@ -376,6 +376,30 @@ class Concat(nn.Module):
 
 
 # =============================================================================== block.py
+def emit_conv3x3_pair(plan, a: "Conv", b: "Conv", x: TV, out: TV | None = None) -> TV:
+    """Conv(c, cm, 3) -> Conv(cm, c, 3) (SiLU both, no shortcut) as one ydbl_bottleneck_nhwc launch with
+    the intermediate in LDS when the (c, cm) pair is built (fp16; used for the Detect box branch
+    cv2[i][0:2] at 64 channels, head.py:86-90), else the two convs."""
+    ca, cb = a.conv, b.conv
+    c, cm = cb.out_channels, ca.out_channels
+    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and (c, cm) == (64, 64)
+          and x.c == c == ca.in_channels and cb.in_channels == cm
+          and all(m.kernel_size == (3, 3) and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1)
+                  and m.groups == 1 for m in (ca, cb))
+          and isinstance(a.act, nn.SiLU) and isinstance(b.act, nn.SiLU))
+    y = out if out is not None else plan.alloc(x.n, x.h, x.w, c)
+    if not ok or y.base is x.base:
+        return b.emit(plan, a.emit(plan, x), out)
+    args = [t.float().contiguous() for t in (*a.folded(), *b.folded())]
+    host = torch.empty(int(_lib.lib.ydbl_conv3x3_pair_params_size(c, cm)), dtype=torch.uint8)
+    _lib.check(_lib.lib.ydbl_conv3x3_pair_pack(*[t.data_ptr() for t in args], c, cm, host.data_ptr()),
+               "ydbl_conv3x3_pair_pack")
+    params = plan.const(host)
+    d = _lib.BottleneckDesc(x.struct(), y.struct(), c, 0, 0, params.data_ptr(), cm)
+    plan.launch("ydbl_bottleneck_nhwc", d, what=f"Conv3x3x2.c{c}", keep=[params, d])
+    return y
+
+
 class Bottleneck(nn.Module):
     """U/nn/modules/block.py:344-357."""
 
@@ -826,8 +850,7 @@ class Detect(nn.Module):
         levels = []
         for i, x in enumerate(xs):
             lv = plan.alloc(x.n, x.h, x.w, self.no)
-            t = self.cv2[i][0].emit(plan, x)
-            t = self.cv2[i][1].emit(plan, t)
+            t = emit_conv3x3_pair(plan, self.cv2[i][0], self.cv2[i][1], x)
             emit_conv2d(plan, self.cv2[i][2], t, lv.cslice(0, 4 * self.reg_max), what="Detect.box")
             if self.legacy:
                 u = self.cv3[i][0].emit(plan, x)
