@@ -432,6 +432,39 @@ def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra, cm):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, rtol=1e-2, atol=1e-2)
 
 
+@pytest.mark.parametrize("n,h,w,cs_extra", [(2, 80, 80, 0), (3, 37, 29, 8), (1, 5, 3, 0)])
+def test_detect_box_fused(n, h, w, cs_extra):
+    """Detect box branch cv2[i] = Conv3x3(64,64) -> Conv3x3(64,64) -> Conv2d 1x1(64,64)+bias (head.py:86-90) as
+    one ydbl_bottleneck_nhwc launch (pw = 1), written into a channel slice of the level buffer; vs fp32
+    convs on fp16-rounded operands with both intermediates rounded to fp16 as the unfused path stores them."""
+    from ydbl import _lib
+
+    torch.manual_seed(n * 100 + h)
+    c = 64
+    x = torch.randn(n, c, h, w)
+    w1, b1 = torch.randn(c, c, 3, 3) / (9 * c) ** 0.5, torch.randn(c) * 0.5
+    w2, b2 = torch.randn(c, c, 3, 3) / (9 * c) ** 0.5, torch.randn(c) * 0.5
+    w3, b3 = torch.randn(c, c) / c ** 0.5, torch.randn(c) * 0.5
+    h16 = lambda t: t.half().float()
+    m1 = h16(F.silu(F.conv2d(h16(x), h16(w1), b1, 1, 1)))
+    m2 = h16(F.silu(F.conv2d(m1, h16(w2), b2, 1, 1)))
+    ref = F.conv2d(m2, h16(w3).reshape(c, c, 1, 1), b3)
+    plan = _plan(torch.float16)
+    xv = _tv_from_nchw(plan, x, cs_extra=cs_extra)
+    lv = plan.alloc(n, h, w, c + 8)  # level buffer [box 64 | cls], box written as a channel slice
+    lv.torch().zero_()
+    yv = lv.cslice(0, c)
+    host = torch.empty(int(_lib.lib.ydbl_detect_box_params_size(c)), dtype=torch.uint8)
+    _lib.check(_lib.lib.ydbl_detect_box_pack(*[t.contiguous().data_ptr() for t in (w1, b1, w2, b2, w3, b3)], c,
+                                             host.data_ptr()))
+    params = host.to(DEV)
+    d = _lib.BottleneckDesc(xv.struct(), yv.struct(), c, 0, 0, params.data_ptr(), c, 1)
+    plan.launch("ydbl_bottleneck_nhwc", d)
+    _run(plan)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, rtol=1e-2, atol=1e-2)
+    assert torch.count_nonzero(lv.torch()[..., c:].float()) == 0  # the class slice is untouched
+
+
 def test_bottleneck_rejects_bad_shapes():
     import ctypes
 

@@ -121,7 +121,7 @@ __device__ __forceinline__ int kbase(int g) {
   return CH >= 4 ? g * PL * 16 : 0;
 }
 
-template <int C, int CMID, int TH, bool ADD>
+template <int C, int CMID, int TH, bool ADD, bool PW = false>
 __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, DView<_Float16> y,
                                                        const unsigned char* __restrict__ params, int tiles_x,
                                                        int tiles_y, int ntiles) {
@@ -238,7 +238,14 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = float(rv[q]) + v[q];
     }
-    store_f<4>(y.at(img, oy, ox) + c2, v);
+    if constexpr (PW) {  // cv2 output, rounded to fp16 as the unfused path stores it, -> LDS for the 1x1
+      h4 o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (_Float16)v[q];
+      *reinterpret_cast<h4*>(s_in + ((c2 >> 3) * (TH * 16) + j * 16 + r16) * 16 + (c2 & 7) * 2) = o;
+    } else {
+      store_f<4>(y.at(img, oy, ox) + c2, v);
+    }
   };
   constexpr int WPT2 = 4 / NT2;
   for (int j = wave / NT2; j < TH; j += 2 * WPT2) {
@@ -257,6 +264,38 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     }
     epi2(acc0, j);
     if (two) epi2(acc1, j1);
+  }
+
+  if constexpr (PW) {
+    // ---- 4. trailing 1x1 conv C -> C + bias (Detect box branch cv2[i][2], head.py:86-90) over the
+    // TH x 16 cv2 tile now in LDS (C/8 planes of TH*16 records, in the input window's space)
+    static_assert(ADD == false && C % 32 == 0 && (C / 8) * TH * 16 * 16 <= Cfg::IN_BYTES, "pw stage layout");
+    constexpr int NT3 = C / 16, KS3 = C / 32, WPT3 = 4 / NT3;
+    const h8* w3f = reinterpret_cast<const h8*>(b2 + C);
+    const float* b3 = reinterpret_cast<const float*>(w3f + NT3 * KS3 * 64);
+    const int t3 = wave % NT3, c3 = 16 * t3 + 4 * g;
+    h8 a3[KS3];
+#pragma unroll
+    for (int m = 0; m < KS3; ++m) a3[m] = w3f[(t3 * KS3 + m) * 64 + lane];
+    float bias3[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bias3[q] = b3[c3 + q];
+    __syncthreads();
+    for (int j = wave / NT3; j < TH; j += WPT3) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < KS3; ++m) {
+        const h8 bf = *reinterpret_cast<const h8*>(s_in + ((m * 4 + g) * (TH * 16) + j * 16 + r16) * 16);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a3[m], bf, acc, 0, 0, 0);
+      }
+      const int oy = oy0 + j, ox = ox0 + r16;
+      if (oy < y.h && ox < y.w) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = acc[q] + bias3[q];
+        store_f<4>(y.at(img, oy, ox) + c3, v);
+      }
+    }
   }
 }
 
@@ -288,12 +327,39 @@ extern "C" int ydbl_conv3x3_pair_pack(const float* w1, const float* b1, const fl
   return fail(YDBL_EINVAL, "bottleneck_pack: (c, c_mid) must be (16, 8), (32, 16), (64, 32) or (64, 64)");
 }
 
+// Detect box branch: the (64, 64) pair blob + the trailing 1x1's A fragments (k = 32m + 8g + j ->
+// input channel, row = output channel) and its fp32 bias
+extern "C" int64_t ydbl_detect_box_params_size(int32_t c) {
+  if (c != 64) return -1;
+  return BneckCfg<64, 64, 16>::BYTES + (64 / 16) * (64 / 32) * 64 * 16 + 64 * 4;
+}
+
+extern "C" int ydbl_detect_box_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                                    const float* b3, int32_t c, void* out) {
+  if (c != 64) return fail(YDBL_EINVAL, "detect_box_pack: c must be 64");
+  if (!w3 || !b3) return fail(YDBL_EINVAL, "detect_box_pack: null pointer");
+  const int r = ydbl_conv3x3_pair_pack(w1, b1, w2, b2, 64, 64, out);
+  if (r) return r;
+  _Float16* f3 = reinterpret_cast<_Float16*>(reinterpret_cast<unsigned char*>(out) + BneckCfg<64, 64, 16>::BYTES);
+  constexpr int NT3 = 4, KS3 = 2;
+  for (int t = 0; t < NT3; ++t)
+    for (int m = 0; m < KS3; ++m)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int co = 16 * t + (lane & 15), ci = (m * 4 + (lane >> 4)) * 8 + j;
+          f3[((t * KS3 + m) * 64 + lane) * 8 + j] = (_Float16)w3[co * 64 + ci];
+        }
+  float* fb3 = reinterpret_cast<float*>(f3 + NT3 * KS3 * 64 * 8);
+  for (int i = 0; i < 64; ++i) fb3[i] = b3[i];
+  return 0;
+}
+
 extern "C" int ydbl_bottleneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c,
                                     void* out) {
   return ydbl_conv3x3_pair_pack(w1, b1, w2, b2, c, c / 2, out);
 }
 
-template <int C, int CMID, int TH>
+template <int C, int CMID, int TH, bool PW = false>
 static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
   using Cfg = BneckCfg<C, CMID, TH>;
   const int tiles_x = (int)cdiv(d->y.w, Cfg::TW), tiles_y = (int)cdiv(d->y.h, TH);
@@ -302,7 +368,9 @@ static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
   auto x = dview<const _Float16>(d->x);
   auto y = dview<_Float16>(d->y);
   auto* p = reinterpret_cast<const unsigned char*>(d->params);
-  if (d->add)
+  if constexpr (PW)
+    bneck_kernel<C, CMID, TH, false, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
+  else if (d->add)
     bneck_kernel<C, CMID, TH, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
   else
     bneck_kernel<C, CMID, TH, false><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
@@ -336,7 +404,12 @@ extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream)
   if (c == 64 && cm == 32) return bneck_dispatch<64, 32>(d, s);
   if (c == 64 && cm == 64) {
     if (d->tile_h == 16) return fail(YDBL_EINVAL, "bottleneck: c_mid 64 takes 8-row tiles only");
+    if (d->pw) {
+      if (d->add) return fail(YDBL_EINVAL, "bottleneck: pw (trailing 1x1) excludes the residual add");
+      return bneck_go<64, 64, 8, true>(d, s);
+    }
     return bneck_go<64, 64, 8>(d, s);
   }
+  if (d->pw) return fail(YDBL_EINVAL, "bottleneck: pw needs (c, c_mid) = (64, 64)");
   return fail(YDBL_EINVAL, "bottleneck: (c, c_mid) must be (16, 8), (32, 16), (64, 32) or (64, 64)");
 }

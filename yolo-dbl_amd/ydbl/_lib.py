@@ -84,7 +84,7 @@ class Stem2Desc(C.Structure):
 
 class BottleneckDesc(C.Structure):
     _fields_ = [("x", View), ("y", View), ("c", C.c_int32), ("add", C.c_int32), ("tile_h", C.c_int32),
-                ("params", C.c_void_p), ("c_mid", C.c_int32)]
+                ("params", C.c_void_p), ("c_mid", C.c_int32), ("pw", C.c_int32)]
 
 
 class LetterboxDesc(C.Structure):
@@ -130,6 +130,8 @@ SIGNATURES = {
     "ydbl_bottleneck_nhwc": ([C.POINTER(BottleneckDesc), _P], C.c_int),
     "ydbl_conv3x3_pair_params_size": ([C.c_int32, C.c_int32], C.c_int64),
     "ydbl_conv3x3_pair_pack": ([_P, _P, _P, _P, C.c_int32, C.c_int32, _P], C.c_int),
+    "ydbl_detect_box_params_size": ([C.c_int32], C.c_int64),
+    "ydbl_detect_box_pack": ([_P, _P, _P, _P, _P, _P, C.c_int32, _P], C.c_int),
     "ydbl_letterbox": ([C.POINTER(LetterboxDesc), _P], C.c_int),
     "ydbl_match_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_match_predictions": ([C.POINTER(MatchDesc), _P], C.c_int),

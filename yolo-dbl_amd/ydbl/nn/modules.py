@@ -400,6 +400,32 @@ def emit_conv3x3_pair(plan, a: "Conv", b: "Conv", x: TV, out: TV | None = None) 
     return y
 
 
+def emit_detect_box(plan, seq, x: TV, out: TV) -> bool:
+    """Detect box branch cv2[i] = Conv(64,64,3) -> Conv(64,64,3) -> Conv2d(64,64,1,bias) (head.py:86-90) as
+    one ydbl_bottleneck_nhwc launch (desc.pw = 1: both 3x3 intermediates stay in LDS).  False (nothing
+    emitted) when the level is not the 64-channel fp16 case."""
+    a, b, c = seq[0], seq[1], seq[2]
+    ca, cb = a.conv, b.conv
+    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and x.c == 64
+          and ca.in_channels == ca.out_channels == cb.in_channels == cb.out_channels == 64
+          and all(m.kernel_size == (3, 3) and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1)
+                  and m.groups == 1 for m in (ca, cb))
+          and isinstance(a.act, nn.SiLU) and isinstance(b.act, nn.SiLU)
+          and isinstance(c, nn.Conv2d) and c.kernel_size == (1, 1) and c.groups == 1 and c.bias is not None
+          and c.in_channels == c.out_channels == 64 and out.c == 64 and out.base is not x.base)
+    if not ok:
+        return False
+    args = [t.float().contiguous() for t in (*a.folded(), *b.folded())]
+    args += [c.weight.detach().float().reshape(64, 64).contiguous(), c.bias.detach().float().contiguous()]
+    host = torch.empty(int(_lib.lib.ydbl_detect_box_params_size(64)), dtype=torch.uint8)
+    _lib.check(_lib.lib.ydbl_detect_box_pack(*[t.data_ptr() for t in args], 64, host.data_ptr()),
+               "ydbl_detect_box_pack")
+    params = plan.const(host)
+    d = _lib.BottleneckDesc(x.struct(), out.struct(), 64, 0, 0, params.data_ptr(), 64, 1)
+    plan.launch("ydbl_bottleneck_nhwc", d, what="Detect.box3", keep=[params, d])
+    return True
+
+
 class Bottleneck(nn.Module):
     """U/nn/modules/block.py:344-357."""
 
@@ -850,8 +876,9 @@ class Detect(nn.Module):
         levels = []
         for i, x in enumerate(xs):
             lv = plan.alloc(x.n, x.h, x.w, self.no)
-            t = emit_conv3x3_pair(plan, self.cv2[i][0], self.cv2[i][1], x)
-            emit_conv2d(plan, self.cv2[i][2], t, lv.cslice(0, 4 * self.reg_max), what="Detect.box")
+            if not emit_detect_box(plan, self.cv2[i], x, lv.cslice(0, 4 * self.reg_max)):
+                t = emit_conv3x3_pair(plan, self.cv2[i][0], self.cv2[i][1], x)
+                emit_conv2d(plan, self.cv2[i][2], t, lv.cslice(0, 4 * self.reg_max), what="Detect.box")
             if self.legacy:
                 u = self.cv3[i][0].emit(plan, x)
                 u = self.cv3[i][1].emit(plan, u)
