@@ -692,6 +692,35 @@ def test_decode_matches_detect_inference(nc):
         sc = ref[b, 4:]  # [nc, A]
         j, a = torch.where(sc > 0.5)
         assert got == sorted((a * nc + j).tolist())
+    # without the reference-layout output the kernel skips the DFL box for non-candidate anchors:
+    # same candidates, boxes and scores (multi-label), and single-label = best class per anchor
+    def cands(multi):
+        cb2, cs2 = torch.empty_like(cb), torch.empty_like(cs)
+        cc2, ci2, cn2 = torch.empty_like(cc), torch.empty_like(ci), torch.empty_like(cn)
+        d2 = _lib.DecodeDesc((_lib.View * 3)(*[lv.cslice(0, 64).struct() for lv in levels]),
+                             (_lib.View * 3)(*[lv.cslice(64, nc).struct() for lv in levels]), 3, nc,
+                             (C.c_float * 3)(8, 16, 32), 0.5, multi, None, 0, None, cb2.data_ptr(), cs2.data_ptr(),
+                             cc2.data_ptr(), ci2.data_ptr(), cn2.data_ptr(), cap)
+        p2 = Plan(torch.device(DEV), torch.float32)
+        p2.launch("ydbl_detect_decode", d2, keep=[d2])
+        _run(p2)
+        return cb2, cs2, cc2, ci2, cn2
+
+    cb2, cs2, cc2, ci2, cn2 = cands(1)
+    for b in range(2):
+        n = cn[b].item()
+        assert cn2[b].item() == n
+        o1, o2 = torch.argsort(ci[b, :n]), torch.argsort(ci2[b, :n])
+        assert torch.equal(ci[b, :n][o1], ci2[b, :n][o2]) and torch.equal(cs[b, :n][o1], cs2[b, :n][o2])
+        assert torch.equal(cb[b, :n][o1], cb2[b, :n][o2])
+    cb2, cs2, cc2, ci2, cn2 = cands(0)
+    for b in range(2):
+        best, bj = ref[b, 4:].max(0)
+        keep = torch.where(best > 0.5)[0]
+        n = cn2[b].item()
+        assert sorted(ci2[b, :n].tolist()) == keep.tolist()
+        o = torch.argsort(ci2[b, :n])
+        assert torch.equal(cc2[b, :n][o].cpu().long(), bj[keep])
 
 
 def _rand_pred(n, nc, A, seed, ties=False):
