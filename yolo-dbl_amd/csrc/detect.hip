@@ -47,26 +47,6 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
   const int loc = a - a0;
   const DView<const T>& bx = p.box[l];
   const int gx = loc % bx.w, gy = loc / bx.w;
-  const T* cp = p.cls[l].at(b, gy, gx);
-  // Class scores first: ~1-2 % of anchors pass the confidence filter, and without the reference-layout
-  // output (yref) the others need no DFL box at all.  Scores are recomputed below with the same
-  // expression, so the candidates are unchanged.
-  if (!p.yref) {
-    bool any = false;
-    float best0 = -1.f;
-    int bj0 = 0;
-    for (int j = 0; j < p.nc; ++j) {
-      const float sc = 1.0f / (1.0f + expf(-float(cp[j])));
-      if (p.multi) {
-        any = any || (sc > p.conf && class_ok(j, p.classes, p.ncls));
-      } else if (sc > best0) {
-        best0 = sc;
-        bj0 = j;
-      }
-    }
-    if (!p.multi) any = best0 > p.conf && class_ok(bj0, p.classes, p.ncls);
-    if (!any) return;
-  }
   const T* bp = bx.at(b, gy, gx);
   float dist[4];
 #pragma unroll
@@ -100,6 +80,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
   // xywh2xyxy (U/utils/ops.py:416-433)
   const float hw = w / 2.0f, hh = h / 2.0f;
   const float bx1 = cx - hw, by1 = cy - hh, bx2 = cx + hw, by2 = cy + hh;
+  const T* cp = p.cls[l].at(b, gy, gx);
   float best = -1.f;
   int bj = 0;
   for (int j = 0; j < p.nc; ++j) {
