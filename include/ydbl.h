@@ -282,11 +282,11 @@ int ydbl_bottleneck_pack(const float* w1, const float* b1, const float* w2, cons
 int64_t ydbl_conv3x3_pair_params_size(int32_t c, int32_t c_mid);
 int ydbl_conv3x3_pair_pack(const float* w1, const float* b1, const float* w2, const float* b2, int32_t c,
                            int32_t c_mid, void* out);
-/* Detect box branch of one level at 64 channels, cv2[i] = Conv3x3 -> Conv3x3 -> Conv2d 1x1 (+bias)
- * (nn/modules/head.py:86-90), as one launch: desc.c = desc.c_mid = 64, desc.pw = 1. */
-int64_t ydbl_detect_box_params_size(int32_t c);
+/* Detect box branch of one level, cv2[i] = Conv3x3(c_in,64) -> Conv3x3(64,64) -> Conv2d 1x1(64,64)+bias
+ * (nn/modules/head.py:86-90), as one launch: desc.c = desc.c_mid = 64, desc.pw = 1, x.c = c_in in {64, 128}. */
+int64_t ydbl_detect_box_params_size(int32_t c_in, int32_t c);
 int ydbl_detect_box_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
-                         const float* b3, int32_t c, void* out);
+                         const float* b3, int32_t c_in, int32_t c, void* out);
 int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream);
 
 /* LetterBox a batch of HWC uint8 BGR frames into one fp32 NCHW RGB canvas batch (values /255).

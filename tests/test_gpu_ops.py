@@ -432,17 +432,18 @@ def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra, cm):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("n,h,w,cs_extra", [(2, 80, 80, 0), (3, 37, 29, 8), (1, 5, 3, 0)])
-def test_detect_box_fused(n, h, w, cs_extra):
-    """Detect box branch cv2[i] = Conv3x3(64,64) -> Conv3x3(64,64) -> Conv2d 1x1(64,64)+bias (head.py:86-90) as
+@pytest.mark.parametrize("cin,n,h,w,cs_extra", [(64, 2, 80, 80, 0), (64, 3, 37, 29, 8), (64, 1, 5, 3, 0),
+                                               (128, 2, 40, 40, 0), (128, 3, 21, 19, 8), (128, 1, 3, 7, 0)])
+def test_detect_box_fused(cin, n, h, w, cs_extra):
+    """Detect box branch cv2[i] = Conv3x3(cin,64) -> Conv3x3(64,64) -> Conv2d 1x1(64,64)+bias (head.py:86-90) as
     one ydbl_bottleneck_nhwc launch (pw = 1), written into a channel slice of the level buffer; vs fp32
     convs on fp16-rounded operands with both intermediates rounded to fp16 as the unfused path stores them."""
     from ydbl import _lib
 
-    torch.manual_seed(n * 100 + h)
+    torch.manual_seed(n * 100 + h + cin)
     c = 64
-    x = torch.randn(n, c, h, w)
-    w1, b1 = torch.randn(c, c, 3, 3) / (9 * c) ** 0.5, torch.randn(c) * 0.5
+    x = torch.randn(n, cin, h, w)
+    w1, b1 = torch.randn(c, cin, 3, 3) / (9 * cin) ** 0.5, torch.randn(c) * 0.5
     w2, b2 = torch.randn(c, c, 3, 3) / (9 * c) ** 0.5, torch.randn(c) * 0.5
     w3, b3 = torch.randn(c, c) / c ** 0.5, torch.randn(c) * 0.5
     h16 = lambda t: t.half().float()
@@ -454,8 +455,8 @@ def test_detect_box_fused(n, h, w, cs_extra):
     lv = plan.alloc(n, h, w, c + 8)  # level buffer [box 64 | cls], box written as a channel slice
     lv.torch().zero_()
     yv = lv.cslice(0, c)
-    host = torch.empty(int(_lib.lib.ydbl_detect_box_params_size(c)), dtype=torch.uint8)
-    _lib.check(_lib.lib.ydbl_detect_box_pack(*[t.contiguous().data_ptr() for t in (w1, b1, w2, b2, w3, b3)], c,
+    host = torch.empty(int(_lib.lib.ydbl_detect_box_params_size(cin, c)), dtype=torch.uint8)
+    _lib.check(_lib.lib.ydbl_detect_box_pack(*[t.contiguous().data_ptr() for t in (w1, b1, w2, b2, w3, b3)], cin, c,
                                              host.data_ptr()))
     params = host.to(DEV)
     d = _lib.BottleneckDesc(xv.struct(), yv.struct(), c, 0, 0, params.data_ptr(), c, 1)

@@ -55,9 +55,9 @@ constexpr int ksteps() {
 }
 constexpr int rup16(int v) { return (v + 15) / 16 * 16; }
 
-template <int C, int CMID, int TH>
+template <int C, int CMID, int TH, int CIN = C>
 struct BneckCfg {
-  static constexpr int CM = CMID, CH = C / 8, CHM = (CM + 7) / 8;
+  static constexpr int CM = CMID, CH = CIN / 8, CHM = (CM + 7) / 8;  // CH: 8-channel chunks of the input
   static constexpr int NT1 = (CM + 15) / 16, NT2 = C / 16;
   static constexpr int KS1 = ksteps<CH>(), KS2 = ksteps<CHM>();
   static constexpr int TW = 16;
@@ -79,9 +79,9 @@ struct BneckCfg {
 
 // Host: fp32 PyTorch-layout weights (BN folded) -> fragment blob.  A[row][k]: row = output channel of
 // the 16-channel tile, k = 32m + 8g + j -> (kslot(m, g), channel chunk*8 + j).
-template <int C, int CMID>
+template <int C, int CMID, int CIN = C>
 void bneck_pack(const float* w1, const float* b1, const float* w2, const float* b2, unsigned char* out) {
-  using Cfg = BneckCfg<C, CMID, 16>;
+  using Cfg = BneckCfg<C, CMID, 16, CIN>;
   constexpr int CM = Cfg::CM;
   _Float16* f1 = reinterpret_cast<_Float16*>(out);
   _Float16* f2 = f1 + Cfg::W1F * 8;
@@ -94,7 +94,7 @@ void bneck_pack(const float* w1, const float* b1, const float* w2, const float* 
           const KSlot s = kslot<Cfg::CH>(m, lane >> 4);
           const int co = 16 * t + (lane & 15), ci = s.chunk * 8 + j;
           const bool ok = s.live && co < CM;
-          f1[((t * Cfg::KS1 + m) * 64 + lane) * 8 + j] = (_Float16)(ok ? w1[(co * C + ci) * 9 + s.tap] : 0.f);
+          f1[((t * Cfg::KS1 + m) * 64 + lane) * 8 + j] = (_Float16)(ok ? w1[(co * CIN + ci) * 9 + s.tap] : 0.f);
         }
   for (int t = 0; t < Cfg::NT2; ++t)
     for (int m = 0; m < Cfg::KS2; ++m)
@@ -121,12 +121,14 @@ __device__ __forceinline__ int kbase(int g) {
   return CH >= 4 ? g * PL * 16 : 0;
 }
 
-template <int C, int CMID, int TH, bool ADD, bool PW = false>
+template <int C, int CMID, int TH, bool ADD, bool PW = false, int CIN = C>
 __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, DView<_Float16> y,
                                                        const unsigned char* __restrict__ params, int tiles_x,
                                                        int tiles_y, int ntiles) {
-  using Cfg = BneckCfg<C, CMID, TH>;
+  using Cfg = BneckCfg<C, CMID, TH, CIN>;
   constexpr int CH = Cfg::CH, CHM = Cfg::CHM, CM = Cfg::CM;
+  static_assert(CIN == C || !ADD, "the residual needs c_in == c");
+  constexpr bool LATE_A2 = CIN > C;  // deep input: cv2's A fragments are loaded after cv1 (VGPR budget)
   constexpr int IP = Cfg::IP, MP = Cfg::MP, PIN = Cfg::PIN, PMID = Cfg::PMID;
   constexpr int NT1 = Cfg::NT1, NT2 = Cfg::NT2, KS1 = Cfg::KS1, KS2 = Cfg::KS2;
   const h8* w1f = reinterpret_cast<const h8*>(params);
@@ -167,8 +169,10 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
   h8 a1[KS1], a2[KS2];
 #pragma unroll
   for (int m = 0; m < KS1; ++m) a1[m] = w1f[(t1 * KS1 + m) * 64 + lane];
+  if constexpr (!LATE_A2) {
 #pragma unroll
-  for (int m = 0; m < KS2; ++m) a2[m] = w2f[(t2 * KS2 + m) * 64 + lane];
+    for (int m = 0; m < KS2; ++m) a2[m] = w2f[(t2 * KS2 + m) * 64 + lane];
+  }
   unsigned char* s_dst = s_in + (s_chunk * PIN + px0) * 16;
 #pragma unroll
   for (int u = 0; u < IT; ++u)
@@ -224,6 +228,10 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
 
   const unsigned char* res_r = s_in + ((c2 >> 3) * PIN + 2 * IP + 2) * 16 + (c2 & 7) * 2;
   const unsigned char* mid_b = s_mid + kbase<CHM, PMID>(g);
+  if constexpr (LATE_A2) {
+#pragma unroll
+    for (int m = 0; m < KS2; ++m) a2[m] = w2f[(t2 * KS2 + m) * 64 + lane];
+  }
   __syncthreads();
 
   // ---- 3. cv2: output rows j, j + WPT2 of the tile, 16 columns = the 16 lanes
@@ -327,20 +335,25 @@ extern "C" int ydbl_conv3x3_pair_pack(const float* w1, const float* b1, const fl
   return fail(YDBL_EINVAL, "bottleneck_pack: (c, c_mid) must be (16, 8), (32, 16), (64, 32) or (64, 64)");
 }
 
-// Detect box branch: the (64, 64) pair blob + the trailing 1x1's A fragments (k = 32m + 8g + j ->
-// input channel, row = output channel) and its fp32 bias
-extern "C" int64_t ydbl_detect_box_params_size(int32_t c) {
-  if (c != 64) return -1;
-  return BneckCfg<64, 64, 16>::BYTES + (64 / 16) * (64 / 32) * 64 * 16 + 64 * 4;
+// Detect box branch: the (c_in -> 64 -> 64) pair blob + the trailing 1x1's A fragments (k = 32m + 8g + j
+// -> input channel, row = output channel) and its fp32 bias.  c_in 64 (P3 of DBL-n), 128 (P4).
+template <int CIN>
+static int64_t box_bytes() {
+  return BneckCfg<64, 64, 16, CIN>::BYTES + (64 / 16) * (64 / 32) * 64 * 16 + 64 * 4;
 }
 
-extern "C" int ydbl_detect_box_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
-                                    const float* b3, int32_t c, void* out) {
-  if (c != 64) return fail(YDBL_EINVAL, "detect_box_pack: c must be 64");
-  if (!w3 || !b3) return fail(YDBL_EINVAL, "detect_box_pack: null pointer");
-  const int r = ydbl_conv3x3_pair_pack(w1, b1, w2, b2, 64, 64, out);
-  if (r) return r;
-  _Float16* f3 = reinterpret_cast<_Float16*>(reinterpret_cast<unsigned char*>(out) + BneckCfg<64, 64, 16>::BYTES);
+extern "C" int64_t ydbl_detect_box_params_size(int32_t c_in, int32_t c) {
+  if (c != 64) return -1;
+  if (c_in == 64) return box_bytes<64>();
+  if (c_in == 128) return box_bytes<128>();
+  return -1;
+}
+
+template <int CIN>
+static void box_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                     const float* b3, unsigned char* out) {
+  bneck_pack<64, 64, CIN>(w1, b1, w2, b2, out);
+  _Float16* f3 = reinterpret_cast<_Float16*>(out + BneckCfg<64, 64, 16, CIN>::BYTES);
   constexpr int NT3 = 4, KS3 = 2;
   for (int t = 0; t < NT3; ++t)
     for (int m = 0; m < KS3; ++m)
@@ -351,6 +364,15 @@ extern "C" int ydbl_detect_box_pack(const float* w1, const float* b1, const floa
         }
   float* fb3 = reinterpret_cast<float*>(f3 + NT3 * KS3 * 64 * 8);
   for (int i = 0; i < 64; ++i) fb3[i] = b3[i];
+}
+
+extern "C" int ydbl_detect_box_pack(const float* w1, const float* b1, const float* w2, const float* b2, const float* w3,
+                                    const float* b3, int32_t c_in, int32_t c, void* out) {
+  if (!w1 || !b1 || !w2 || !b2 || !w3 || !b3 || !out) return fail(YDBL_EINVAL, "detect_box_pack: null pointer");
+  if (c != 64 || (c_in != 64 && c_in != 128)) return fail(YDBL_EINVAL, "detect_box_pack: (c_in, c) must be (64|128, 64)");
+  auto* o = reinterpret_cast<unsigned char*>(out);
+  if (c_in == 64) box_pack<64>(w1, b1, w2, b2, w3, b3, o);
+  else box_pack<128>(w1, b1, w2, b2, w3, b3, o);
   return 0;
 }
 
@@ -359,9 +381,9 @@ extern "C" int ydbl_bottleneck_pack(const float* w1, const float* b1, const floa
   return ydbl_conv3x3_pair_pack(w1, b1, w2, b2, c, c / 2, out);
 }
 
-template <int C, int CMID, int TH, bool PW = false>
+template <int C, int CMID, int TH, bool PW = false, int CIN = C>
 static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
-  using Cfg = BneckCfg<C, CMID, TH>;
+  using Cfg = BneckCfg<C, CMID, TH, CIN>;
   const int tiles_x = (int)cdiv(d->y.w, Cfg::TW), tiles_y = (int)cdiv(d->y.h, TH);
   const int64_t nt = (int64_t)tiles_x * tiles_y * d->y.n;
   if (nt > 0x7fffffff) return fail(YDBL_EINVAL, "bottleneck: grid too large");
@@ -369,7 +391,7 @@ static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
   auto y = dview<_Float16>(d->y);
   auto* p = reinterpret_cast<const unsigned char*>(d->params);
   if constexpr (PW)
-    bneck_kernel<C, CMID, TH, false, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
+    bneck_kernel<C, CMID, TH, false, true, CIN><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
   else if (d->add)
     bneck_kernel<C, CMID, TH, true><<<(unsigned)nt, 256, 0, s>>>(x, y, p, tiles_x, tiles_y, (int)nt);
   else
@@ -392,7 +414,9 @@ extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream)
   if (check_view(&d->x, "bottleneck.x", true) || check_view(&d->y, "bottleneck.y", true)) return YDBL_EINVAL;
   if (d->x.dtype != YDBL_F16 || d->y.dtype != YDBL_F16) return fail(YDBL_EINVAL, "bottleneck: fp16 views only");
   const int c = d->c, cm = d->c_mid ? d->c_mid : d->c / 2;
-  if (d->x.c != c || d->y.c != c) return fail(YDBL_EINVAL, "bottleneck: x.c and y.c must equal c");
+  const int cin = d->x.c;
+  if (d->y.c != c || (cin != c && !(d->pw && cin == 128)))
+    return fail(YDBL_EINVAL, "bottleneck: y.c must equal c, and x.c too (except x.c 128 with pw)");
   if (d->x.n != d->y.n || d->x.h != d->y.h || d->x.w != d->y.w)
     return fail(YDBL_EINVAL, "bottleneck: x and y shapes differ");
   if (d->y.n < 1 || d->y.h < 1 || d->y.w < 1) return fail(YDBL_EINVAL, "bottleneck: empty input");
@@ -406,7 +430,7 @@ extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream)
     if (d->tile_h == 16) return fail(YDBL_EINVAL, "bottleneck: c_mid 64 takes 8-row tiles only");
     if (d->pw) {
       if (d->add) return fail(YDBL_EINVAL, "bottleneck: pw (trailing 1x1) excludes the residual add");
-      return bneck_go<64, 64, 8, true>(d, s);
+      return cin == 128 ? bneck_go<64, 64, 8, true, 128>(d, s) : bneck_go<64, 64, 8, true>(d, s);
     }
     return bneck_go<64, 64, 8>(d, s);
   }

@@ -130,8 +130,8 @@ SIGNATURES = {
     "ydbl_bottleneck_nhwc": ([C.POINTER(BottleneckDesc), _P], C.c_int),
     "ydbl_conv3x3_pair_params_size": ([C.c_int32, C.c_int32], C.c_int64),
     "ydbl_conv3x3_pair_pack": ([_P, _P, _P, _P, C.c_int32, C.c_int32, _P], C.c_int),
-    "ydbl_detect_box_params_size": ([C.c_int32], C.c_int64),
-    "ydbl_detect_box_pack": ([_P, _P, _P, _P, _P, _P, C.c_int32, _P], C.c_int),
+    "ydbl_detect_box_params_size": ([C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_detect_box_pack": ([_P, _P, _P, _P, _P, _P, C.c_int32, C.c_int32, _P], C.c_int),
     "ydbl_letterbox": ([C.POINTER(LetterboxDesc), _P], C.c_int),
     "ydbl_match_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_match_predictions": ([C.POINTER(MatchDesc), _P], C.c_int),

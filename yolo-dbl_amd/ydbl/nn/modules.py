@@ -401,13 +401,13 @@ def emit_conv3x3_pair(plan, a: "Conv", b: "Conv", x: TV, out: TV | None = None) 
 
 
 def emit_detect_box(plan, seq, x: TV, out: TV) -> bool:
-    """Detect box branch cv2[i] = Conv(64,64,3) -> Conv(64,64,3) -> Conv2d(64,64,1,bias) (head.py:86-90) as
+    """Detect box branch cv2[i] = Conv(c_in,64,3) -> Conv(64,64,3) -> Conv2d(64,64,1,bias) (head.py:86-90) as
     one ydbl_bottleneck_nhwc launch (desc.pw = 1: both 3x3 intermediates stay in LDS).  False (nothing
-    emitted) when the level is not the 64-channel fp16 case."""
+    emitted) unless fp16 with c_in 64 or 128 (DBL-n P3 / P4)."""
     a, b, c = seq[0], seq[1], seq[2]
     ca, cb = a.conv, b.conv
-    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and x.c == 64
-          and ca.in_channels == ca.out_channels == cb.in_channels == cb.out_channels == 64
+    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and x.c in (64, 128)
+          and ca.in_channels == x.c and ca.out_channels == cb.in_channels == cb.out_channels == 64
           and all(m.kernel_size == (3, 3) and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1)
                   and m.groups == 1 for m in (ca, cb))
           and isinstance(a.act, nn.SiLU) and isinstance(b.act, nn.SiLU)
@@ -417,8 +417,8 @@ def emit_detect_box(plan, seq, x: TV, out: TV) -> bool:
         return False
     args = [t.float().contiguous() for t in (*a.folded(), *b.folded())]
     args += [c.weight.detach().float().reshape(64, 64).contiguous(), c.bias.detach().float().contiguous()]
-    host = torch.empty(int(_lib.lib.ydbl_detect_box_params_size(64)), dtype=torch.uint8)
-    _lib.check(_lib.lib.ydbl_detect_box_pack(*[t.data_ptr() for t in args], 64, host.data_ptr()),
+    host = torch.empty(int(_lib.lib.ydbl_detect_box_params_size(x.c, 64)), dtype=torch.uint8)
+    _lib.check(_lib.lib.ydbl_detect_box_pack(*[t.data_ptr() for t in args], x.c, 64, host.data_ptr()),
                "ydbl_detect_box_pack")
     params = plan.const(host)
     d = _lib.BottleneckDesc(x.struct(), out.struct(), 64, 0, 0, params.data_ptr(), 64, 1)
