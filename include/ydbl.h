@@ -114,6 +114,12 @@ typedef struct {
   int32_t kpad, act, res_mode;
   const float* dw_bias;
   int32_t dw_act;
+  /* optional trailing 1x1 conv (Detect cls conv cv3[i][2], head.py:93-101) over y's 64 channels:
+   * tail_y[p][k] = sum_c tail_w[k][c] * y[p][c] + tail_b[k], k < tail_n <= 4 (y is still written) */
+  const float* tail_w;
+  const float* tail_b;
+  ydbl_view tail_y;
+  int32_t tail_n;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 

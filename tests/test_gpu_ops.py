@@ -260,13 +260,52 @@ def test_detect_dw_pw_fused(dtype, c, c2, shape):
     x = torch.randn(*shape)
     plan = _plan(dtype)
     xv = _tv_from_nchw(plan, x)
-    y = M.emit_dw_pw(plan, dwc, pwc, xv)
+    y, _ = M.emit_dw_pw(plan, dwc, pwc, xv)
     assert [st.fn.__name__ for st in plan.steps] == ["ydbl_dsconv_nhwc"]
     _run(plan)
     with torch.no_grad():
         r = ref(x.to(dtype).float())
     tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
     torch.testing.assert_close(y.nchw().float().cpu(), r, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("nc,shape", [(3, (2, 64, 40, 40)), (1, (1, 64, 13, 17)), (4, (3, 64, 80, 80))])
+def test_detect_cls_tail_fused(dtype, nc, shape):
+    """Detect cv3[i][1] pair DWConv(64,64,3) -> Conv(64,64,1) plus the class conv cv3[i][2] = Conv2d(64,nc,1,bias)
+    (head.py:93-101) in one launch: the class logits land in the level buffer's class slice."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(nc * 10 + shape[2])
+    ref = torch.nn.Sequential(om.DWConv(64, 64, 3), om.Conv(64, 64, 1)).eval()
+    cls = torch.nn.Conv2d(64, nc, 1)
+    with torch.no_grad():
+        for bn in [m for m in ref.modules() if isinstance(m, torch.nn.BatchNorm2d)]:
+            bn.running_mean.uniform_(-0.2, 0.2)
+            bn.running_var.uniform_(0.5, 2.0)
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    dwc, pwc = M.DWConv(64, 64, 3), M.Conv(64, 64, 1)
+    dwc.load_state_dict(ref[0].state_dict())
+    pwc.load_state_dict(ref[1].state_dict())
+    x = torch.randn(*shape)
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x)
+    n, _, h, w = shape
+    lv = plan.alloc(n, h, w, 64 + nc)
+    lv.torch().zero_()
+    y, done = M.emit_dw_pw(plan, dwc, pwc, xv, tail_conv=cls, tail_out=lv.cslice(64, nc))
+    assert done and [st.fn.__name__ for st in plan.steps] == ["ydbl_dsconv_nhwc"]
+    _run(plan)
+    with torch.no_grad():
+        u = ref(x.to(dtype).float()).to(dtype).float()  # the pair's output as the unfused path stores it
+        r = torch.nn.functional.conv2d(u, cls.weight.to(dtype).float() if dtype == torch.float16 else cls.weight,
+                                       cls.bias)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(y.nchw().float().cpu(), u, **tol)
+    torch.testing.assert_close(lv.cslice(64, nc).nchw().float().cpu(), r, **tol)
+    assert torch.count_nonzero(lv.torch()[..., :64].float()) == 0  # box slice untouched
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])

@@ -22,6 +22,10 @@ struct ConvArgs {
   // and the accumulator is dequantized by dq[co] = 1 / (sw[co] * qs) before bias / activation.
   const float* dq;
   float qs;
+  // optional trailing 1x1 conv of nt3 (<= 4) outputs over all Cout channels (dsconv.hip, Detect cls):
+  // y3[p][k] = sum_c t3w[k][c] * T(y[p][c]) + t3b[k]
+  const float* t3w; const float* t3b;
+  T* y3; int y3cs; int nt3;
 };
 
 // ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------
@@ -168,6 +172,46 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
           for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) y2p[q] = T(p.a2 * float(T(v[q])) + p.b2 * float(r2p[q]));
         }
       }
+    }
+  }
+}
+
+// Trailing 1x1 conv with <= 4 outputs over all Cout channels of a pixel, for kernels whose wave holds
+// every channel of its pixels (TN * 16 == Cout): the Detect head's class conv cv3[i][2] (head.py:93-101)
+// after its DWConv -> Conv1x1 pair.  Lane (r16, g) holds channels co[i]..co[i]+3 of pixel pp[j]; the
+// rounded activations (T, as the unfused path stores them) are dotted with the weights per lane and the
+// four lane groups are summed by xor-shuffles (fixed order); lane group 0 stores.
+template <typename T, int TN, int TM>
+__device__ __forceinline__ void conv_tail_1x1(const ConvArgs<T>& p, const f32x4 (&acc)[TN][TM], const int64_t (&pp)[TM],
+                                              const bool (&pv)[TM], const int (&co)[TN], int g) {
+  float bv[TN][4], wv[TN][4][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      bv[i][q] = p.bias ? p.bias[co[i] + q] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv[i][q][k] = k < p.nt3 ? p.t3w[k * p.Cout + co[i] + q] : 0.f;
+    }
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float u = float(T(apply_act(acc[i][j][q] + bv[i][q], p.act)));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) part[k] = fmaf(u, wv[i][q][k], part[k]);
+      }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      part[k] += __shfl_xor(part[k], 16);
+      part[k] += __shfl_xor(part[k], 32);
+    }
+    if (g == 0 && pv[j]) {
+      T* o = p.y3 + pp[j] * p.y3cs;
+      for (int k = 0; k < p.nt3; ++k) o[k] = T(part[k] + p.t3b[k]);
     }
   }
 }

@@ -207,6 +207,9 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
   conv_epilogue<T, NTN, TMW>(p, acc, pp, pv, co);
+  if constexpr (NTN == 4) {  // the tail is only launched with Cout 64 = NTN * 16 (host-checked)
+    if (p.t3w) conv_tail_1x1<T, NTN, TMW>(p, acc, pp, pv, co, g);
+  }
 }
 
 template <typename T, int K, int S, int DIL, int TH, int TW, int CSEG, bool DBUF = true>
@@ -218,7 +221,7 @@ static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, const float* 
     kern<<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y, cs);
   };
   static const char* fn = getenv("YDBL_DS_NTN");  // A/B knob for scripts/ds_bench.py: force 2/4 output tiles
-  const int force = fn && *fn ? atoi(fn) : 0;
+  const int force = fn && *fn && !a.t3w ? atoi(fn) : 0;  // the tail needs every channel in one wave
   if (force == 2) return go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
   if (force == 4) return go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
   if (a.Cout <= 32) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
@@ -255,6 +258,10 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
   a.KW = d->k; a.S = d->stride; a.PAD = d->pad; a.DIL = d->dil;
   a.K = d->x.c; a.KPAD = d->kpad;
   a.act = d->act; a.res = d->res_mode;
+  if (d->tail_w) {
+    a.t3w = d->tail_w; a.t3b = d->tail_b; a.nt3 = d->tail_n;
+    a.y3 = reinterpret_cast<T*>(d->tail_y.ptr); a.y3cs = d->tail_y.cs;
+  }
   a.P = d->y.n * d->y.h * d->y.w;
   if (d->k == 3 && d->stride == 1 && d->dil == 1) return launch_ds<T, 3, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
   if (d->k == 3 && d->stride == 2 && d->dil == 1) return launch_ds<T, 3, 2, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
@@ -284,6 +291,12 @@ extern "C" int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream) {
     if (d->r.cs % 4 || d->r.dtype != d->y.dtype || d->r.n != d->y.n || d->r.h != d->y.h || d->r.w != d->y.w ||
         d->r.c < d->y.c)
       return fail(YDBL_EINVAL, "dsconv: residual shape mismatch");
+  }
+  if (d->tail_w) {
+    if (!d->tail_b || d->tail_n < 1 || d->tail_n > 4 || d->y.c != 64 || d->res_mode != YDBL_RES_NONE ||
+        check_view(&d->tail_y, "dsconv.tail_y", false) || d->tail_y.c != d->tail_n || d->tail_y.dtype != d->y.dtype ||
+        d->tail_y.n != d->y.n || d->tail_y.h != d->y.h || d->tail_y.w != d->y.w)
+      return fail(YDBL_EINVAL, "dsconv: tail needs y.c 64, 1 <= tail_n <= 4, tail_y [n,h,w,tail_n] of y's dtype, no residual");
   }
   const hipStream_t s = as_stream(stream);
   return d->x.dtype == YDBL_F16 ? run_ds<_Float16>(d, s) : run_ds<float>(d, s);

@@ -44,7 +44,8 @@ class DsConvDesc(C.Structure):
     _fields_ = [("x", View), ("y", View), ("r", View), ("dw_w", C.c_void_p), ("pw_w", C.c_void_p),
                 ("bias", C.c_void_p), ("k", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
                 ("dil", C.c_int32), ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32),
-                ("dw_bias", C.c_void_p), ("dw_act", C.c_int32)]
+                ("dw_bias", C.c_void_p), ("dw_act", C.c_int32), ("tail_w", C.c_void_p), ("tail_b", C.c_void_p),
+                ("tail_y", View), ("tail_n", C.c_int32)]
 
 
 class HgDesc(C.Structure):

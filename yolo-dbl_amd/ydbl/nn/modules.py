@@ -162,9 +162,11 @@ def fused_dsconv_ok(dw: nn.Conv2d, x: TV, dtype) -> bool:
 
 def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Tensor, b_pw: torch.Tensor,
                 act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv",
-                w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE) -> TV:
+                w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE,
+                tail: tuple | None = None) -> TV:
     """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA.
-    w_dw / b_dw / dw_act: folded DWConv weights, bias and activation (Detect's DWConv -> Conv1x1 pair)."""
+    w_dw / b_dw / dw_act: folded DWConv weights, bias and activation (Detect's DWConv -> Conv1x1 pair).
+    tail = (w [n, co], b [n], out view): a trailing 1x1 conv with n <= 4 outputs in the same launch."""
     k, st, p, d = dw.kernel_size[0], dw.stride[0], dw.padding[0], dw.dilation[0]
     c = x.c
     co = w_pw.shape[0]
@@ -177,24 +179,39 @@ def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Te
     pww = plan.const(torch.nn.functional.pad(w_pw.reshape(co, c).float(), (0, kpad - c)).to(plan.dtype))
     bd = plan.const(b_pw.float())
     dwb = plan.const(b_dw.float()) if b_dw is not None else None
+    tw = tb = None
+    tail_args = (None, None, _null_view(), 0)
+    if tail is not None:
+        tw, tb = plan.const(tail[0].float().contiguous()), plan.const(tail[1].float().contiguous())
+        tail_args = (tw.data_ptr(), tb.data_ptr(), tail[2].struct(), tail[2].c)
+        what += "+1x1"
     desc = _lib.DsConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(),
                            dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode,
-                           dwb.data_ptr() if dwb is not None else None, dw_act)
-    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, dwb, desc])
+                           dwb.data_ptr() if dwb is not None else None, dw_act, *tail_args)
+    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, dwb, tw, tb, desc])
     return y
 
 
-def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = None, what="DWConv+Conv1x1") -> TV:
+def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = None, what="DWConv+Conv1x1",
+               tail_conv: nn.Conv2d | None = None, tail_out: TV | None = None):
     """nn.Sequential(DWConv(c, c, k), Conv(c, c2, 1)) of the Detect head (head.py:93-101): one fused launch
-    when the shapes allow (the depthwise output stays in LDS), else two."""
+    when the shapes allow (the depthwise output stays in LDS), else two.  With tail_conv (the class conv
+    cv3[i][2], 1x1 c2 -> nc, bias) the launch also writes tail_out when c2 == 64 and nc <= 4; returns
+    (y, tail_done)."""
     if fused_dsconv_ok(dwc.conv, x, plan.dtype) and pwc.conv.kernel_size == (1, 1) and pwc.conv.stride == (1, 1):
         wd, bdw = dwc.folded()
         wp, bp = pwc.folded()
         if bdw is None:
             bdw = torch.zeros(x.c)
-        return emit_dsconv(plan, dwc.conv, x, out, wp, bp if bp is not None else torch.zeros(wp.shape[0]),
-                           _act_code(pwc.act), what=what, w_dw=wd, b_dw=bdw, dw_act=_act_code(dwc.act))
-    return pwc.emit(plan, dwc.emit(plan, x), out)
+        tail = None
+        if (tail_conv is not None and wp.shape[0] == 64 and tail_conv.kernel_size == (1, 1) and tail_conv.groups == 1
+                and tail_conv.in_channels == 64 and 1 <= tail_conv.out_channels <= 4 and tail_conv.bias is not None):
+            nc = tail_conv.out_channels
+            tail = (tail_conv.weight.detach().float().reshape(nc, 64), tail_conv.bias.detach().float(), tail_out)
+        y = emit_dsconv(plan, dwc.conv, x, out, wp, bp if bp is not None else torch.zeros(wp.shape[0]),
+                        _act_code(pwc.act), what=what, w_dw=wd, b_dw=bdw, dw_act=_act_code(dwc.act), tail=tail)
+        return y, tail is not None
+    return pwc.emit(plan, dwc.emit(plan, x), out), False
 
 
 def stem_ok(m, ch: int) -> bool:
@@ -882,9 +899,15 @@ class Detect(nn.Module):
             if self.legacy:
                 u = self.cv3[i][0].emit(plan, x)
                 u = self.cv3[i][1].emit(plan, u)
-            else:  # [DWConv, Conv1x1] x 2: each pair is one fused depthwise -> pointwise launch
-                u = emit_dw_pw(plan, self.cv3[i][0][0], self.cv3[i][0][1], x)
-                u = emit_dw_pw(plan, self.cv3[i][1][0], self.cv3[i][1][1], u)
+            else:  # [DWConv, Conv1x1] x 2: each pair is one fused depthwise -> pointwise launch; the class conv
+                # cv3[i][2] (64 -> nc <= 4) rides in the second pair's epilogue
+                cls_out = lv.cslice(4 * self.reg_max, self.nc)
+                u, _ = emit_dw_pw(plan, self.cv3[i][0][0], self.cv3[i][0][1], x)
+                u, done = emit_dw_pw(plan, self.cv3[i][1][0], self.cv3[i][1][1], u, tail_conv=self.cv3[i][2],
+                                     tail_out=cls_out)
+                if done:
+                    levels.append(lv)
+                    continue
             emit_conv2d(plan, self.cv3[i][2], u, lv.cslice(4 * self.reg_max, self.nc), what="Detect.cls")
             levels.append(lv)
         return levels
