@@ -151,6 +151,39 @@ def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("n,cin,cout,h,w,res", [
+    (8, 64, 64, 320, 320, None),      # >= 204800 output pixels (DBL-l backbone-like)
+    (4, 64, 96, 642, 322, "add"),     # odd input width, ragged tiles, partial second channel split
+])
+def test_conv3x3_halo_s2(dtype, n, cin, cout, h, w, res):
+    """3x3 stride-2 convs with >= 204800 output pixels: the halo-tiled kernel with S = 2."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + cout + h + 2)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 2, 1))
+    ho, wo = ref.shape[2:]
+    assert n * ho * wo >= 204800
+    plan = _plan(dtype)
+    xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+    ybuf = plan.alloc(n, ho, wo, cout + 8)
+    yv = ybuf.cslice(8, cout)
+    rv, mode = None, _lib.RES_NONE
+    if res:
+        r = torch.randn(n, cout, ho, wo)
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD
+        ref = r.to(dtype).float() + ref
+    emit_dense(plan, xv, yv, wt, b, 2, 1, 1, _lib.ACT_SILU, rv, mode)
+    _run(plan)
+    tol = _tol(dtype) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
+
+
 @pytest.mark.parametrize("n,cin,cout,h,w,res", [
     (2, 128, 64, 40, 40, "add"),      # 40-wide map: a half-empty last column tile
     (3, 128, 64, 21, 19, "add"),      # ragged 8x16 tiles on both edges

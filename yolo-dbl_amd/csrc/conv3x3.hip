@@ -174,6 +174,13 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
 template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   constexpr int BK = 4 * Vec<T>::N;
+  // Stride 2 on >= 204800 output pixels: 8-row tiles over a (2*8+1) x 33 halo (YDBL_NO_HALO_S2 A/B:
+  // DBL-l 128->256 @320 bs8 442 -> 341 us).  Smaller maps stay on the block GEMM: 128->128 @40 bs32
+  // 17.8 vs 24.7 us, and DBL-n's 64->64 @80 bs32 (18.8 vs 17.5 us alone) cost the whole step ~40 us.
+  static const bool no_s2 = getenv("YDBL_NO_HALO_S2") != nullptr;
+  if (!no_s2 && kh == 3 && a.KW == 3 && a.PAD == 1 && a.DIL == 1 && a.S == 2 && a.Cin % BK == 0 &&
+      a.Cin >= 2 * BK && a.xcs % Vec<T>::N == 0 && (int64_t)a.P >= 204800)
+    return launch_halo<T, Q8, 2, 8>(a, s), true;
   if (kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
   if (a.Cin % BK || a.Cin < 2 * BK || a.xcs % Vec<T>::N) return false;
   static const char* fth = getenv("YDBL_HALO_TH");  // A/B knob for scripts/conv_bench.py: force 4/8/16-row tiles
