@@ -37,7 +37,7 @@
  *                             Conv(3,C0,3,1) -> Conv(C0,2*C0,3,2), conv.py:39-63 after fuse), fp16
  *   ydbl_gate_add          <- FullPAD_Tunnel.forward nn/modules/block.py:1954-1956
  *   ydbl_pool_up_concat    <- FuseModule.forward block.py:1831-1840, DownsampleConv block.py:1927
- *   ydbl_dysample          <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
+ *   ydbl_dysample(_ex)     <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
  *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
  *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708
  *   ydbl_detect_decode     <- Detect._inference head.py:143-181 + DFL block.py:79-83 +
@@ -162,6 +162,15 @@ int ydbl_pool_up_concat(const ydbl_view* p_lo, const ydbl_view* p_mid, const ydb
 /* DySample 'lp' x2 sampling: off fp32 view [n,h,w,8*groups] holding 0.25*offset+init_pos
  * (channel k = coord*4g + group*4 + i*2 + j), bilinear border grid_sample of x into y [n,2h,2w,c]. */
 int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y, void* stream);
+/* Same, descriptor form with an optional second output (y2.ptr != NULL): y2 = a2 * y + b2 * r2 -- a
+ * FullPAD_Tunnel (nn/modules/block.py:1954-1956) fed by this DySample, fused into its epilogue. */
+typedef struct {
+  ydbl_view x, off;
+  int32_t groups;
+  ydbl_view y, y2, r2;
+  float a2, b2;
+} ydbl_dysample_desc;
+int ydbl_dysample_ex(const ydbl_dysample_desc* d, void* stream);
 
 /* LSKblock gate: attn view = [a1 | a2] (2*half channels, each half = dim/2);
  * agg = [mean_c, max_c](attn); sig = sigmoid(conv7x7(agg) + sb); out = a1*sig0 + a2*sig1.

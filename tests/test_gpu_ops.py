@@ -379,6 +379,44 @@ def test_fullpad_fused_into_conv(dtype, late):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_fullpad_fused_into_dysample(dtype):
+    """FullPAD_Tunnel fed by a DySample (DBL L16 = FullPAD(x7, DySample(x12))) becomes the DySample launch's
+    second output: no gate_add launch, y = x0 + gate * x1 and the DySample output itself unchanged."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(11)
+    o = om.DySample(64).eval()
+    with torch.no_grad():
+        o.offset.weight.normal_(0, 0.3)
+        o.offset.bias.normal_(0, 1.0)
+    ds = M.DySample(64)
+    ds.load_state_dict(o.state_dict())
+    pad, opad = M.FullPAD_Tunnel(), om.FullPAD_Tunnel()
+    with torch.no_grad():
+        opad.gate.fill_(0.61)
+    pad.load_state_dict(opad.state_dict())
+    x = torch.randn(2, 64, 9, 7)
+    z = torch.randn(2, 32, 18, 14)
+    ca, oca = M.Conv(32, 64, 1).eval(), om.Conv(32, 64, 1).eval()  # x0 comes from an earlier conv launch
+    ca.load_state_dict(oca.state_dict())
+    plan = _plan(dtype)
+    xv, zv = _tv_from_nchw(plan, x), _tv_from_nchw(plan, z)
+    av = ca.emit(plan, zv)
+    y = ds.emit(plan, xv)
+    out = pad.emit(plan, [av, y])
+    assert not any(st.what == "FullPAD" for st in plan.steps)
+    _run(plan)
+    with torch.no_grad():
+        ry = o(x.to(dtype).float())
+        ra = oca(z.to(dtype).float())
+        ref = opad([ra.to(dtype).float(), ry.to(dtype).float()])
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(y.nchw().float().cpu(), ry, **tol)
+    torch.testing.assert_close(out.nchw().float().cpu(), ref, **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("c,k,s,d,bias,res", [(16, 3, 1, 1, False, False), (32, 3, 2, 1, True, False),
                                              (64, 7, 1, 1, False, True), (24, 5, 1, 1, True, False),
                                              (16, 7, 1, 3, True, False), (16, 3, 1, 2, False, False),

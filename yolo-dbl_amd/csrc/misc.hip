@@ -369,7 +369,8 @@ __global__ __launch_bounds__(256) void pool_up_concat_kernel(DView<const T> lo, 
 // offset channel k = coord*4G + group*4 + i*2 + j (i,j = sub-pixel row/col of the x2 output).
 // Coordinates follow DySample.py:48-61 and ATen grid_sampler (align_corners=False, border).
 template <typename T>
-__global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<const T> off, int G, DView<T> y) {
+__global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<const T> off, int G, DView<T> y,
+                                                       DView<T> y2, DView<const T> r2, float a2, float b2) {
   constexpr int V = Vec<T>::N;
   const int cpg = x.c / G;
   const int cgv = cpg / V;
@@ -424,6 +425,13 @@ __global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<c
     acc[q] += vse[q] * kse;
   }
   store_f<V>(y.at(b, oy2, ox2) + c0, acc);
+  if (y2.p) {  // fused FullPAD_Tunnel (block.py:1954-1956) on this output: y2 = a2 * T(y) + b2 * r2
+    float rv[V], o2[V];
+    load_f<V>(r2.at(b, oy2, ox2) + c0, rv);
+#pragma unroll
+    for (int q = 0; q < V; ++q) o2[q] = a2 * float(T(acc[q])) + b2 * rv[q];
+    store_f<V>(y2.at(b, oy2, ox2) + c0, o2);
+  }
 }
 
 // ------------------------------------------------------------------ LSKblock gate
@@ -644,8 +652,8 @@ extern "C" int ydbl_pool_up_concat(const ydbl_view* lo, const ydbl_view* mid, co
   return check_launch("ydbl_pool_up_concat");
 }
 
-extern "C" int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y,
-                             void* stream) {
+static int dysample_go(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y,
+                       const ydbl_view* y2, const ydbl_view* r2, float a2, float b2, void* stream) {
   if (check_view(x, "dysample.x", true) || check_view(off, "dysample.off", false) || check_view(y, "dysample.y", true))
     return YDBL_EINVAL;
   const int V = y->dtype == YDBL_F16 ? 8 : 4;
@@ -653,14 +661,35 @@ extern "C" int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t g
   if (off->c != 8 * groups || off->h != x->h || off->w != x->w || y->h != 2 * x->h || y->w != 2 * x->w ||
       y->c != x->c || off->dtype != x->dtype || y->dtype != x->dtype)
     return fail(YDBL_EINVAL, "dysample: shape mismatch");
+  const bool two = y2 && y2->ptr;
+  if (two) {
+    if (check_view(y2, "dysample.y2", true) || check_view(r2, "dysample.r2", true)) return YDBL_EINVAL;
+    auto same = [&](const ydbl_view* v) {
+      return v->n == y->n && v->h == y->h && v->w == y->w && v->c == y->c && v->dtype == y->dtype;
+    };
+    if (!same(y2) || !same(r2)) return fail(YDBL_EINVAL, "dysample: y2/r2 must match y");
+  }
   hipStream_t s = as_stream(stream);
   const int64_t total = (int64_t)y->n * y->h * y->w * groups * (x->c / groups / V);
   if (y->dtype == YDBL_F16)
-    dysample_kernel<_Float16><<<nblk(total), 256, 0, s>>>(cview<_Float16>(x), cview<_Float16>(off), groups,
-                                                           dview<_Float16>(*y));
+    dysample_kernel<_Float16><<<nblk(total), 256, 0, s>>>(
+        cview<_Float16>(x), cview<_Float16>(off), groups, dview<_Float16>(*y),
+        two ? dview<_Float16>(*y2) : DView<_Float16>{nullptr, 0, 0, 0, 0, 0}, cview<_Float16>(two ? r2 : nullptr), a2, b2);
   else
-    dysample_kernel<float><<<nblk(total), 256, 0, s>>>(cview<float>(x), cview<float>(off), groups, dview<float>(*y));
+    dysample_kernel<float><<<nblk(total), 256, 0, s>>>(
+        cview<float>(x), cview<float>(off), groups, dview<float>(*y),
+        two ? dview<float>(*y2) : DView<float>{nullptr, 0, 0, 0, 0, 0}, cview<float>(two ? r2 : nullptr), a2, b2);
   return check_launch("ydbl_dysample");
+}
+
+extern "C" int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y,
+                             void* stream) {
+  return dysample_go(x, off, groups, y, nullptr, nullptr, 0.f, 0.f, stream);
+}
+
+extern "C" int ydbl_dysample_ex(const ydbl_dysample_desc* d, void* stream) {
+  if (!d) return fail(YDBL_EINVAL, "dysample: null descriptor");
+  return dysample_go(&d->x, &d->off, d->groups, &d->y, &d->y2, &d->r2, d->a2, d->b2, stream);
 }
 
 extern "C" int64_t ydbl_lsk_gate_workspace(int32_t n, int32_t h, int32_t w) { return (int64_t)n * h * w * 2 * 4; }

@@ -83,6 +83,11 @@ class Stem2Desc(C.Structure):
                 ("scale", C.c_float), ("c0", C.c_int32), ("params", C.c_void_p), ("y", View)]
 
 
+class DySampleDesc(C.Structure):
+    _fields_ = [("x", View), ("off", View), ("groups", C.c_int32), ("y", View), ("y2", View), ("r2", View),
+                ("a2", C.c_float), ("b2", C.c_float)]
+
+
 class BottleneckDesc(C.Structure):
     _fields_ = [("x", View), ("y", View), ("c", C.c_int32), ("add", C.c_int32), ("tile_h", C.c_int32),
                 ("params", C.c_void_p), ("c_mid", C.c_int32), ("pw", C.c_int32)]
@@ -114,6 +119,7 @@ SIGNATURES = {
     "ydbl_gate_add": ([_VP, _VP, C.c_float, _VP, _P], C.c_int),
     "ydbl_pool_up_concat": ([_VP, _VP, _VP, _VP, _P], C.c_int),
     "ydbl_dysample": ([_VP, _VP, C.c_int32, _VP, _P], C.c_int),
+    "ydbl_dysample_ex": ([C.POINTER(DySampleDesc), _P], C.c_int),
     "ydbl_lsk_gate": ([_VP, _P, _P, _VP, _P, _P], C.c_int),
     "ydbl_lsk_gate_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_hg_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),

@@ -803,7 +803,9 @@ class DySample(nn.Module):
         off = plan.alloc(x.n, x.h, x.w, 8 * self.groups)
         emit_conv2d(plan, self.offset, x, off, w, b, what="DySample.offset")
         y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)
-        plan.launch("ydbl_dysample", x.struct(), off.struct(), self.groups, y.struct(), what="DySample.sample")
+        d = _lib.DySampleDesc(x.struct(), off.struct(), self.groups, y.struct(), _null_view(), _null_view(), 0.0, 0.0)
+        plan.launch("ydbl_dysample_ex", d, what="DySample.sample", keep=[d])
+        plan.note_writer(y, d)  # a FullPAD_Tunnel on y becomes this launch's second output
         return y
 
 

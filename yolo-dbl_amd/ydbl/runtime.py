@@ -84,7 +84,7 @@ class Plan:
         self.steps: list[Step] = []
         self.buffers: list[torch.Tensor] = []
         self.bytes_allocated = 0
-        self._writers: dict = {}  # view key -> (step index, ConvDesc) of the dense conv that wrote it
+        self._writers: dict = {}  # view key -> (step index, desc) of the conv / DySample launch that wrote it
         self.fp8_candidates: list = []  # (ConvDesc, input view, fp32 [Cout][KPAD] weights) of fp8-able convs
 
     # ---------------------------------------------------------------- memory
