@@ -19,7 +19,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-_CFG_DIR = Path(__file__).resolve().parent.parent / "yolo-dbl_amd" / "ydbl" / "cfg" / "models"
+# the oracle owns its transcription of the reference YAMLs (U/cfg/models/v13/yolov13_DBL{,2}.yaml);
+# tests/test_oracle.py::test_model_configs_transcribed pins it to the product copy and, where
+# /root/reference exists, to the YAML files themselves
+_CFG_DIR = Path(__file__).resolve().parent / "cfg"
 
 
 # --------------------------------------------------------------------------- helpers

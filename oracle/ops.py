@@ -100,6 +100,8 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
         if not n:
             continue
         if n > max_nms:
+            # the reference calls a non-stable argsort (U/utils/ops.py:286): the order of equal scores is
+            # unspecified there; the restatement (and the GPU kernel) fix it to the stable order
             x = x[x[:, 4].argsort(descending=True, stable=True)[:max_nms]]
         c = x[:, 5:6] * (0 if agnostic else max_wh)
         keep = nms_torchvision(x[:, :4] + c, x[:, 4], iou_thres)[:max_det]

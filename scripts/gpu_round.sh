@@ -8,7 +8,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 [ -n "$SKIP_TESTS" ] || timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" | tee -a $OUT/pytest_gpu.log; tail -5 $OUT/pytest_gpu.log
-[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
+[ $rc -eq 0 ] || { echo "GPU parity tests FAILED (rc=$rc): not running smoke/bench/profile"; exit $rc; }
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail -20 $OUT/smoke.log; exit 3; }
 tail -3 $OUT/smoke.log
 timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 || { echo bench failed; tail -30 $OUT/bench.log; exit 4; }

@@ -1,0 +1,195 @@
+"""Shared helpers for the end-to-end parity tests (test infrastructure; imports oracle/).
+
+The oracle restatement (oracle/model.py) is run in three precisions on the same
+state_dict and the same input:
+- fp64: the BN-folded fp32 weights evaluated in double precision = the "exact"
+  answer of the fused network (the reference fuses BN in fp32 too, U/nn/tasks.py:207-235);
+- fp32: the reference's own CPU path (U/engine/predictor.py:116-134, AutoBackend fp32);
+- fp16: the reference's half=True path (AutoBackend .half(), U/nn/autobackend.py:145-155)
+  evaluated by torch-CPU in float16.
+The GPU result of a precision is then judged against the fp64 answer with a bound
+taken from how far the reference's own path of that precision lands from it.
+"""
+
+from __future__ import annotations
+
+import copy
+import time
+
+import torch
+
+from oracle.metrics import box_iou as box_iou_xyxy
+from oracle.ops import clip_boxes, non_max_suppression
+
+ROLE_FX = {"n": ("yolov13n_DBL.yaml", "trained_yolov13n_DBL_nc{nc}.npz"),
+           "s": ("yolov13s_DBL.yaml", "trained_yolov13s_DBL_nc{nc}.npz"),
+           "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc{nc}.npz")}
+
+
+def build_pair(scale: str, nc: int, golden_dir):
+    """(product YOLO, fused fp32 oracle) with identical weights."""
+    from oracle.model import build_model
+    from ydbl import YOLO
+    from ydbl.utils.synthetic import load_trained
+
+    cfg, fx = ROLE_FX[scale]
+    fx = golden_dir / fx.format(nc=nc)
+    torch.manual_seed(0)
+    p = YOLO(cfg, nc=nc)
+    load_trained(p.model, fx)
+    torch.manual_seed(0)
+    o = build_model(cfg, nc=nc)
+    load_trained(o, fx)
+    o.fuse()
+    return p, o
+
+
+def oracle_only(scale: str, nc: int, golden_dir):
+    """The fused fp32 oracle of a BASELINE model with the trained-like fixture."""
+    from oracle.model import build_model
+    from ydbl.utils.synthetic import load_trained
+
+    cfg, fx = ROLE_FX[scale]
+    torch.manual_seed(0)
+    o = build_model(cfg, nc=nc)
+    load_trained(o, golden_dir / fx.format(nc=nc))
+    return o.fuse()
+
+
+def fp32_rule(st):
+    """(box px, score) tolerance of the fp32 comparison: twice the reference fp32 path's worst deviation
+    from the fp64 answer (st = err_stats of that leg) plus a floor of 1e-3 px / 1e-6."""
+    return 2 * st["box_max"] + 1e-3, 2 * st["conf_max"] + 1e-6
+
+
+def fp16_rule(st):
+    """fp16 tolerance: twice the reference half path's p99.9 deviation from fp64 (its max is dominated by
+    a handful of anchors whose 16-bin DFL softmax is nearly flat)."""
+    return 2 * st["box_p999"] + 1e-2, 2 * st["conf_p999"] + 1e-4
+
+
+def load_e2e(golden_dir, name):
+    import json
+
+    import numpy as np
+
+    with np.load(golden_dir / f"e2e_{name}.npz", allow_pickle=False) as z:
+        return torch.from_numpy(z["y64"]).double(), json.loads(str(z["meta"]))
+
+
+@torch.inference_mode()
+def oracle_legs(o, x, legs=("fp64", "fp32")):
+    """Decoded predictions y[B, 4+nc, A] (fp32 tensors) of the oracle in each precision + seconds."""
+    out, secs = {}, {}
+    for leg in legs:
+        t0 = time.perf_counter()
+        if leg == "fp32":
+            y, _ = o(x)
+        elif leg == "fp64":
+            y, _ = copy.deepcopy(o).double()(x.double())
+        elif leg == "fp16":
+            y, _ = copy.deepcopy(o).half()(x.half())
+        else:
+            raise ValueError(leg)
+        out[leg] = y.float() if leg != "fp64" else y
+        secs[leg] = time.perf_counter() - t0
+    return out, secs
+
+
+def err_stats(y, y64):
+    """max / p99.9 abs deviation of boxes (px) and scores from the fp64 answer."""
+    y = y.double()
+    db = (y[:, :4] - y64[:, :4]).abs().flatten()
+    dc = (y[:, 4:] - y64[:, 4:]).abs().flatten()
+    q = lambda t: torch.quantile(t[torch.randperm(t.numel(), generator=torch.Generator().manual_seed(0))[:1 << 20]],
+                                 0.999).item()
+    return {"box_max": db.max().item(), "box_p999": q(db), "conf_max": dc.max().item(), "conf_p999": q(dc)}
+
+
+def class_agreement(y_gpu, y64, margin):
+    """Anchors whose fp64 top-2 class margin exceeds `margin` must have the same argmax class on the GPU
+    (torch.max first-index rule, U/utils/ops.py:274).  Returns (checked anchors, disagreements)."""
+    nc = y64.shape[1] - 4
+    if nc < 2:
+        return 0, 0
+    s64 = y64[:, 4:]
+    top2 = s64.topk(2, dim=1).values
+    safe = (top2[:, 0] - top2[:, 1]) > margin
+    a = y_gpu[:, 4:].float().argmax(1)
+    b = s64.argmax(1)
+    return int(safe.sum()), int(((a != b) & safe).sum())
+
+
+def detections(y, conf, iou, hw, multi_label=False):
+    dets = non_max_suppression(y.float(), conf, iou, multi_label=multi_label)
+    for d in dets:
+        clip_boxes(d[:, :4], hw)  # predict.py:23-41 postprocess -> scale_boxes -> clip_boxes
+    return dets
+
+
+def _borderline(det, y_ref, conf, iou, tol_box, tol_conf, cut):
+    """True when the NMS decision about `det` ([6]) can flip under perturbations of tol_box / tol_conf:
+    - its score is within tol_conf of the conf threshold, or of the max_det cut (`cut`: the lowest kept
+      score of a full image, U/utils/ops.py:300-301), or
+    - an anchor at its box has top-2 class scores within 2*tol_conf (the class can flip, :274), or
+    - a same-class candidate of comparable-or-higher score overlaps it with an IoU within the IoU change
+      a tol_box move can cause (the torchvision keep decision can flip, :296)."""
+    if det[4] <= conf + tol_conf or det[4] <= cut + tol_conf:
+        return True
+    from oracle.ops import xywh2xyxy
+
+    p = y_ref.float().T  # [A, 4+nc]
+    sc, cl = p[:, 4:].max(1)
+    boxes_all = xywh2xyxy(p[:, :4].clone())
+    if p.shape[1] > 5:
+        near = (boxes_all - det[:4]).abs().amax(1) <= tol_box
+        top2 = p[near, 4:].topk(2, dim=1).values
+        if len(top2) and ((top2[:, 0] - top2[:, 1]) <= 2 * tol_conf).any():
+            return True
+    keep = (sc > conf - tol_conf) & (cl == det[5].long()) & (sc >= det[4] - 2 * tol_conf)
+    if not keep.any():
+        return False
+    ious = box_iou_xyxy(det[None, :4], boxes_all[keep])[0]
+    wh = (det[2:4] - det[0:2]).clamp(min=1.0)
+    d_iou = 4.0 * tol_box / wh.min().item() + 1e-3  # first-order IoU change for a tol_box shift
+    return bool(((ious - iou).abs() <= d_iou).any())
+
+
+def match_detections(ref, got, y_ref, conf, iou, tol_box, tol_conf, max_det=300):
+    """Compare two per-image detection lists both ways: every detection of one set needs a same-class
+    detection in the other within (tol_box px, tol_conf).  An unmatched detection is "borderline" when
+    its NMS decision can flip under that perturbation (_borderline on the reference predictions y_ref
+    [B, 4+nc, A]); anything else is a mismatch.
+    Returns dict(pairs, box_dev, conf_dev, borderline, mismatches=[...])."""
+    out = {"pairs": 0, "box_dev": 0.0, "conf_dev": 0.0, "borderline": 0, "mismatches": []}
+    for b, (r_i, g_i) in enumerate(zip(ref, got)):
+        for a_set, b_set, a_is_ref in ((r_i, g_i, True), (g_i, r_i, False)):
+            cut = a_set[:, 4].min().item() if len(a_set) >= max_det else -1.0
+            for d in a_set:
+                if len(b_set):
+                    same = b_set[:, 5] == d[5]
+                    dev_b = (b_set[:, :4] - d[:4]).abs().amax(1)
+                    dev_c = (b_set[:, 4] - d[4]).abs()
+                    ok = same & (dev_b <= tol_box) & (dev_c <= tol_conf)
+                    if ok.any():
+                        j = torch.where(ok, dev_b, torch.full_like(dev_b, 1e9)).argmin()
+                        out["box_dev"] = max(out["box_dev"], dev_b[j].item())
+                        out["conf_dev"] = max(out["conf_dev"], dev_c[j].item())
+                        out["pairs"] += a_is_ref
+                        continue
+                if _borderline(d, y_ref[b], conf, iou, tol_box, tol_conf, cut):
+                    out["borderline"] += 1
+                else:
+                    out["mismatches"].append(("ref" if a_is_ref else "got", b, [round(v, 3) for v in d.tolist()]))
+    return out
+
+
+def gpu_pred(p, x, half=False, fp8=False, conf=0.25, iou=0.7, calib=None):
+    """Decoded predictions + final detections of the product path (HIP through libydbl)."""
+    B, _, H, W = x.shape
+    s = p.session(B, H, W, half=half, conf=conf, iou=iou, keep_pred=True, use_graph=False, fp8=fp8)
+    if fp8:
+        s.calibrate_fp8((calib if calib is not None else x).cuda())
+    s(x.cuda())
+    torch.cuda.synchronize()
+    return s.pred.cpu(), s.results()

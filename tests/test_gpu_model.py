@@ -1,10 +1,10 @@
-"""End-to-end parity on the MI355X: YOLO(cfg) HIP path vs the oracle restatement.
+"""End-to-end parity on the MI355X at small sizes: YOLO(cfg) HIP path vs the oracle restatement.
 
-Same state_dict (seeded init + tests/golden trained-like fixture), same inputs.
-fp32 mode: the reference's CPU path is fp32; differences come only from the
-accumulation order of ~150 convolutions, so the decoded output is compared with
-a tolerance and the NMS result set by matching.  fp16 mode is judged on
-detection agreement only (as SURVEY.md §7 prescribes).
+Same state_dict (seeded init + tests/golden trained-like fixture), same inputs.  fp32 mode is judged
+against the oracle's fp64 answer with twice the reference fp32 path's own deviation as the bound
+(tests/parity_util.py); the BASELINE shapes (640 / 1280, full batches, fp32 and fp16) are in
+tests/test_gpu_e2e.py.  Also: NMS bit-exactness on the GPU's own decoded output, graph replay, the
+predict() API and the mAP protocol.
 """
 
 import numpy as np
@@ -31,45 +31,39 @@ def _models(cfg, nc, golden_dir):
     return p, o
 
 
-def _match(ref, got, atol):
-    """Every reference box has a same-class GPU box within atol (and vice versa); returns max dev."""
-    if len(ref) == 0 and len(got) == 0:
-        return 0.0
-    assert len(ref) and len(got), (len(ref), len(got))
-    d = (ref[:, None, :5] - got[None, :, :5]).abs().amax(-1)
-    same = ref[:, None, 5] == got[None, :, 5]
-    d = torch.where(same, d, torch.full_like(d, 1e9))
-    return max(d.min(1).values.max().item(), d.min(0).values.max().item())
-
-
 @pytest.mark.parametrize("cfg,nc,size", [("yolov13n_DBL.yaml", 3, 128), ("yolov13n_DBL.yaml", 80, 160),
-                                         ("yolov13s_DBL.yaml", 3, 128), ("yolov13l_DBL2.yaml", 3, 128)])
+                                         ("yolov13s_DBL.yaml", 3, 128), ("yolov13s_DBL.yaml", 80, 160),
+                                         ("yolov13l_DBL2.yaml", 3, 128)])
 def test_model_fp32_parity(cfg, nc, size, golden_dir):
+    """Small-size companion of tests/test_gpu_e2e.py (which runs the BASELINE shapes): raw per-level head
+    outputs, decoded predictions and final detections vs the oracle's fp64 answer, bounded by twice the
+    reference fp32 path's own deviation (parity_util.fp32_rule); nc=80 exercises class-index agreement."""
+    from parity_util import class_agreement, detections, err_stats, fp32_rule, match_detections, oracle_legs
     from ydbl.utils.synthetic import blob_images
 
     p, o = _models(cfg, nc, golden_dir)
     x = blob_images(2, size, seed=1234)
+    ys, _ = oracle_legs(o, x, ("fp64", "fp32"))
+    y64 = ys["fp64"]
     with torch.no_grad():
-        y_ref, feats_ref = o(x)
+        _, feats_ref = o(x)
     s = p.session(2, size, size, half=False, conf=0.05, iou=0.7, keep_pred=True, use_graph=False)
     s(x.cuda())
     torch.cuda.synchronize()
     y = s.pred.cpu()
-    # raw per-level head outputs (reference x[i] layout) and decoded predictions
-    for f_ref, f in zip(feats_ref, s.feats()):
-        err = (f.float().cpu() - f_ref).abs().max().item()
-        assert err < 2e-2, err
-    boxes_err = (y[:, :4] - y_ref[:, :4]).abs().max().item()
-    conf_err = (y[:, 4:] - y_ref[:, 4:]).abs().max().item()
-    print(f"{cfg} nc={nc}: max |dbox| {boxes_err:.3g} px, max |dconf| {conf_err:.3g}")
-    assert conf_err < 1e-3
-    assert boxes_err < 5e-2
-    from oracle.ops import non_max_suppression
-
-    ref = non_max_suppression(y_ref, 0.05, 0.7)
-    got = s.results()
-    for r, g in zip(ref, got):
-        assert abs(len(r) - len(g)) <= max(1, len(r) // 20)
+    for f_ref, f in zip(feats_ref, s.feats()):  # raw per-level head outputs (reference x[i] layout)
+        assert (f.float().cpu() - f_ref).abs().max().item() < 2e-2
+    o32 = err_stats(ys["fp32"], y64)
+    st = err_stats(y, y64)
+    tb, tc = fp32_rule(o32)
+    print(f"{cfg} nc={nc}: gpu |dbox| {st['box_max']:.3g} px, |dconf| {st['conf_max']:.3g}; "
+          f"oracle fp32 {o32['box_max']:.3g} px, {o32['conf_max']:.3g}")
+    assert st["box_max"] <= tb and st["conf_max"] <= tc
+    checked, bad = class_agreement(y, y64, tc)
+    assert bad == 0 and (nc < 2 or checked > 0)
+    ref = detections(y64, 0.05, 0.7, (size, size))
+    m = match_detections(ref, s.results(), y64, 0.05, 0.7, tb, tc)
+    assert not m["mismatches"], m["mismatches"][:5]
 
 
 def test_dbl_n_nms_consistency_fp32(golden_dir):

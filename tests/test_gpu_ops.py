@@ -222,14 +222,16 @@ def test_conv3x3_vw(n, cin, cout, h, w, res):
     assert torch.count_nonzero(full[..., :8]) == 0 and torch.count_nonzero(full[..., 8 + cout:]) == 0
 
 
-@pytest.mark.parametrize("cin,cout,k,n,h,w,res", [
-    (64, 64, 3, 2, 160, 160, "add"),  # halo-tiled kernel (>= 51200 px)
-    (96, 40, 3, 2, 19, 23, None),     # block implicit GEMM, Cout tail
-    (128, 128, 1, 2, 24, 40, "add"),  # pointwise GEMM
-    (128, 64, 3, 1, 20, 20, None),    # K = 1152: wave-split-K
-    (512, 96, 1, 2, 10, 10, None),    # K = 512 on a small map: wave-split-K pointwise
+@pytest.mark.parametrize("cin,cout,k,n,h,w,res,s", [
+    (64, 64, 3, 2, 160, 160, "add", 1),  # halo-tiled kernel (>= 51200 px)
+    (96, 40, 3, 2, 19, 23, None, 1),     # block implicit GEMM, Cout tail
+    (128, 128, 1, 2, 24, 40, "add", 1),  # pointwise GEMM
+    (128, 64, 3, 1, 20, 20, None, 1),    # K = 1152: wave-split-K
+    (512, 96, 1, 2, 10, 10, None, 1),    # K = 512 on a small map: wave-split-K pointwise
+    (64, 64, 3, 8, 320, 320, None, 2),   # stride-2 halo route (>= 204800 output px: 8 x 160 x 160)
+    (64, 48, 3, 2, 37, 45, None, 2),     # stride 2 on the block GEMM, odd map
 ])
-def test_conv_fp8(cin, cout, k, n, h, w, res):
+def test_conv_fp8(cin, cout, k, n, h, w, res, s):
     """e4m3 operands (BASELINE config 5): GPU fp8 MFMA vs a CPU emulation that applies the same
     quantization (per-channel weight scale, calibrated per-tensor activation scale, saturation)."""
     from ydbl import _lib
@@ -242,14 +244,15 @@ def test_conv_fp8(cin, cout, k, n, h, w, res):
     b = torch.randn(cout)
     plan = _plan(torch.float16)
     xv = _tv_from_nchw(plan, x)
-    ybuf = plan.alloc(n, h, w, cout + 8)
+    ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+    ybuf = plan.alloc(n, ho, wo, cout + 8)
     yv = ybuf.cslice(8, cout)
     rv, mode = None, _lib.RES_NONE
-    r = torch.randn(n, cout, h, w)
+    r = torch.randn(n, cout, ho, wo)
     if res:
         rv = _tv_from_nchw(plan, r)
         mode = _lib.RES_ADD
-    emit_dense(plan, xv, yv, wt, b, 1, k // 2, 1, _lib.ACT_SILU, rv, mode)
+    emit_dense(plan, xv, yv, wt, b, s, k // 2, 1, _lib.ACT_SILU, rv, mode)
     assert len(plan.fp8_candidates) == 1
     assert enable_fp8(plan, plan.run) == 1
     _run(plan)
@@ -260,14 +263,14 @@ def test_conv_fp8(cin, cout, k, n, h, w, res):
     w2 = wt.permute(0, 2, 3, 1).reshape(cout, -1)
     wq, sw = quantize_weights_e4m3(w2)
     wdq = wq.view(torch.float8_e4m3fn).float().reshape(cout, k, k, cin).permute(0, 3, 1, 2)
-    acc = F.conv2d(xq, wdq, None, 1, k // 2) / (sw[None, :, None, None] * qs)
+    acc = F.conv2d(xq, wdq, None, s, k // 2) / (sw[None, :, None, None] * qs)
     ref = F.silu(acc + b[None, :, None, None])
     if res:
         ref = r.half().float() + ref
     got = yv.nchw().float().cpu()
     torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
     # and the quantized conv stays close to the exact one (sanity of the scales)
-    exact = F.silu(F.conv2d(x16, wt, b, 1, k // 2)) + (r.half().float() if res else 0)
+    exact = F.silu(F.conv2d(x16, wt, b, s, k // 2)) + (r.half().float() if res else 0)
     assert (got - exact).abs().mean().item() < 0.05
 
 
@@ -663,14 +666,21 @@ def test_lskblock(dtype, c, h, w):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
-@pytest.mark.parametrize("c,edges", [(64, 4), (128, 8)])
-def test_c3ah_hypergraph(dtype, c, edges):
+@pytest.mark.parametrize("c,edges,n,h,w", [
+    (64, 4, 2, 10, 8), (128, 8, 2, 10, 8),
+    # production token counts: the softmax over N runs over ceil(N/256) logits workgroups whose
+    # partial (max, sum) pairs are merged (hg.hip) -- DBL-n/s P4 @640 (N=1600), DBL-l P4 @1280 (N=6400,
+    # 16 heads), and a ragged N=257 (one token in the second workgroup)
+    (64, 4, 2, 40, 40), (128, 8, 2, 40, 40), (256, 8, 1, 80, 80), (64, 4, 1, 1, 257),
+])
+def test_c3ah_hypergraph(dtype, c, edges, n, h, w):
+    """AdaHyperedgeGen softmax over tokens (U/nn/modules/block.py:1652-1657) and AdaHGConv propagation."""
     from oracle import model as om
     from ydbl.nn import modules as M
 
     torch.manual_seed(5)
     o = om.C3AH(c, c, 1, edges).eval()
-    x = torch.randn(2, c, 10, 8)
+    x = torch.randn(n, c, h, w)
     tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
     _module_parity(o, M.C3AH(c, c, 1, edges), [x], dtype, tol)
 

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <type_traits>
 
 #include "../../include/ydbl.h"
 
@@ -140,15 +141,20 @@ __device__ __forceinline__ void store_f(float* p, const float* v) {
 // ---- activations (fp32) ---------------------------------------------------------------------
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
-// SiLU in the conv epilogues: hardware exp2 + reciprocal (v_exp_f32 / v_rcp_f32, ~1 ulp each)
-// instead of the IEEE expf + division sequence; 4-5 VALU ops per element, within the fp32
-// parity tolerance and far below fp16 rounding.
+// SiLU in the fp16 / fp8 epilogues: hardware exp2 + reciprocal (v_exp_f32 / v_rcp_f32, ~1 ulp
+// each) instead of the IEEE expf + division sequence; 4-5 VALU ops per element, far below fp16
+// rounding.  The fp32 (parity) path keeps ATen's CPU op sequence x / (1 + exp(-x)) with IEEE
+// division, so its only deviation from the reference is the accumulation order of the convs.
 __device__ __forceinline__ float silu_fast(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-v * 1.4426950408889634f));
 }
+__device__ __forceinline__ float silu_exact(float v) { return v / (1.0f + expf(-v)); }
+template <typename T>
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
-    case YDBL_ACT_SILU: return silu_fast(v);
+    case YDBL_ACT_SILU:
+      if constexpr (std::is_same<T, float>::value) return silu_exact(v);
+      else return silu_fast(v);
     case YDBL_ACT_GELU: return gelu_erf(v);
     case YDBL_ACT_SIGMOID: return sigmoidf_(v);
     default: return v;

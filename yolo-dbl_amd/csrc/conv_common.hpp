@@ -144,7 +144,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
     for (int i = 0; i < TN; ++i) {
       float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[i][j][q] * dqv[i][q] + bv[i][q], p.act);
+      for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] * dqv[i][q] + bv[i][q], p.act);
       if (p.res == YDBL_RES_ADD) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = rv[i][q] + v[q];
@@ -200,7 +200,7 @@ __device__ __forceinline__ void conv_tail_1x1(const ConvArgs<T>& p, const f32x4 
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float u = float(T(apply_act(acc[i][j][q] + bv[i][q], p.act)));
+        const float u = float(T(apply_act<T>(acc[i][j][q] + bv[i][q], p.act)));
 #pragma unroll
         for (int k = 0; k < 4; ++k) part[k] = fmaf(u, wv[i][q][k], part[k]);
       }

@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
 #pragma unroll
         for (int c = 0; c < CSEG; ++c)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) a[c][e] = apply_act(a[c][e] + bq[e], dw_act);
+          for (int e = 0; e < 4; ++e) a[c][e] = apply_act<T>(a[c][e] + bq[e], dw_act);
       }
 #pragma unroll
       for (int c = 0; c < CSEG; ++c) {

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DView<const T> x, DView<T> 
     for (int q = 0; q < V; ++q) acc[q] += bv[q];
   }
 #pragma unroll
-  for (int q = 0; q < V; ++q) acc[q] = apply_act(acc[q], act);
+  for (int q = 0; q < V; ++q) acc[q] = apply_act<T>(acc[q], act);
   if (r.p) {
     float rv[V];
     load_f<V>(r.at(b, oy, ox) + c0, rv);
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void dwconv_lds_kernel(DView<const T> x, DView
     const int oy = oy0 + py[u], ox = ox0 + px[u];
     float o[V];
 #pragma unroll
-    for (int q = 0; q < V; ++q) o[q] = apply_act(bias ? acc[u][q] + bv[q] : acc[u][q], act);
+    for (int q = 0; q < V; ++q) o[q] = apply_act<T>(bias ? acc[u][q] + bv[q] : acc[u][q], act);
     if (r.p) {
       float rv[V];
       load_f<V>(r.at(b, oy, ox) + cc, rv);
@@ -227,7 +227,7 @@ __device__ __forceinline__ void dw_pair_phase(const typename Vec<T>::type* src, 
     }
     float o[V];
 #pragma unroll
-    for (int q = 0; q < V; ++q) o[q] = apply_act(bias ? acc[q] + bv[q] : acc[q], act);
+    for (int q = 0; q < V; ++q) o[q] = apply_act<T>(bias ? acc[q] + bv[q] : acc[q], act);
     store_f<V>(out.at(b, oy, ox) + cc, o);
     if (keep) {
       vec t;

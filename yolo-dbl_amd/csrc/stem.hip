@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
       if (co >= y.c) continue;
       float v[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(acc[t][q] + bv[t][q], act);
+      for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[t][q] + bv[t][q], act);
       store_f<4>(yp + co, v);
     }
   }
