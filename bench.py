@@ -106,11 +106,27 @@ def pmc_traffic():
     return None
 
 
-def cpu_baseline(model_key, imgsz, budget_s=15.0):
-    """Oracle (CPU restatement of the reference path, fp32) on a bounded sample: forward + NMS per image."""
+def _cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(model_key, imgsz, batch, budget_s=10.0, gpu_session=None):
+    """The oracle (CPU restatement of the reference path, fp32, BN folded as fuse() does) timed on this
+    box's host cores over bounded samples of the same workload: forward + decode +
+    NMS (conf .25, iou .7) + clip per image.
+      leg 1: all intra-op threads, bs = the GPU batch (the headline `value`);
+      leg 2: 1 thread (the reference's import-time OMP_NUM_THREADS=1 default, U/__init__.py:9-10), bs=1.
+    Also the accuracy half of the metric: mAP@0.5 of the GPU path vs the CPU path on a fixed labelled
+    set (pseudo ground truth = CPU detections at conf .25), when gpu_session is given."""
     sys.path.insert(0, str(ROOT))
     from oracle.model import build_model
-    from oracle.ops import non_max_suppression
+    from oracle.ops import clip_boxes, non_max_suppression
     from ydbl.utils.synthetic import blob_images, load_trained
 
     cfg, fx = CFGS[model_key]
@@ -118,20 +134,107 @@ def cpu_baseline(model_key, imgsz, budget_s=15.0):
     m = build_model(cfg, nc=3)
     load_trained(m, ROOT / "tests" / "golden" / fx)
     m.fuse()
-    x = blob_images(1, imgsz, seed=1234)
+    threads_all = torch.get_num_threads()
+
+    def leg(bs, threads):
+        torch.set_num_threads(threads)
+        x = blob_images(bs, imgsz, seed=1234)
+        with torch.inference_mode():
+            def once():
+                y, _ = m(x)
+                for d in non_max_suppression(y, 0.25, 0.7):
+                    clip_boxes(d[:, :4], (imgsz, imgsz))
+            once()  # warm-up
+            n, t0 = 0, time.perf_counter()
+            while True:
+                once()
+                n += 1
+                el = time.perf_counter() - t0
+                if el > budget_s or n >= 50:
+                    break
+        return {"img_per_s": round(n * bs / el, 3), "bs": bs, "threads": threads, "iters": n, "secs": round(el, 1)}
+
+    legs = [leg(batch, threads_all), leg(1, 1)]
+    torch.set_num_threads(threads_all)
+    out = {"value": legs[0]["img_per_s"], "unit": "images/s", "cores": threads_all, "kind": "port",
+           "sample": f"{legs[0]['iters']} x bs{batch} DBL-{model_key} {imgsz}x{imgsz} nc3 fp32 oracle forward+NMS "
+                     f"on {threads_all} threads ({legs[0]['secs']} s); 1-thread leg: {legs[1]['img_per_s']} img/s",
+           "legs": legs, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
+    if gpu_session is not None:
+        out["map50"] = accuracy_check(m, gpu_session, imgsz)
+    return out
+
+
+def accuracy_check(m, gpu, imgsz, n=8):
+    """|mAP50_gpu - mAP50_cpu| on n blob images with pseudo ground truth (SURVEY §8d protocol; the same
+    val pipeline -- conf .001, multi-label NMS, iou .7 -- scores both paths)."""
+    from oracle.metrics import IOUV, box_iou, match_predictions
+    from oracle.ops import clip_boxes, non_max_suppression
+    from ydbl.utils.metrics import DetMetrics
+    from ydbl.utils.synthetic import blob_images
+
+    x = blob_images(n, imgsz, seed=321)
     with torch.inference_mode():
-        y, _ = m(x)  # warm-up
-        non_max_suppression(y, 0.25, 0.7)
-        n, t0 = 0, time.perf_counter()
-        while True:
-            y, _ = m(x)
-            non_max_suppression(y, 0.25, 0.7)
-            n += 1
-            el = time.perf_counter() - t0
-            if el > budget_s or n >= 200:
-                break
-    return {"value": round(n / el, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} images of {imgsz}x{imgsz}, bs=1, fp32 oracle forward+NMS ({el:.1f}s)"}
+        y, _ = m(x)
+    labels = []
+    for g in non_max_suppression(y, 0.25, 0.7):
+        clip_boxes(g[:, :4], (imgsz, imgsz))
+        labels.append(torch.cat([g[:, 5:6], g[:, :4]], 1))
+    st = {"tp": [], "conf": [], "pred_cls": [], "target_cls": []}
+    for i, p in enumerate(non_max_suppression(y, 0.001, 0.7, multi_label=True)):
+        clip_boxes(p[:, :4], (imgsz, imgsz))
+        cls, box = labels[i][:, 0], labels[i][:, 1:]
+        tp = (match_predictions(p[:, 5], cls, box_iou(box, p[:, :4]), IOUV) if len(cls) and len(p)
+              else torch.zeros(len(p), 10, dtype=torch.bool))
+        st["tp"].append(tp); st["conf"].append(p[:, 4]); st["pred_cls"].append(p[:, 5]); st["target_cls"].append(cls)
+    dm = DetMetrics()
+    dm.process(*(torch.cat(st[k]).numpy() for k in ("tp", "conf", "pred_cls", "target_cls")))
+    batch = {"img": x, "cls": torch.cat([lb[:, 0] for lb in labels]), "bboxes": torch.cat([lb[:, 1:] for lb in labels]),
+             "batch_idx": torch.cat([torch.full((len(lb),), i) for i, lb in enumerate(labels)])}
+    yolo, fp8 = gpu  # the product YOLO (HIP path) and whether the bench runs e4m3 operands
+    m_gpu = yolo.val(data=[batch], half=True, fp8=fp8).box.map50
+    return {"gpu": round(float(m_gpu), 4), "cpu": round(float(dm.box.map50), 4),
+            "drop": round(float(dm.box.map50 - m_gpu), 4),
+            "images": n, "gt_boxes": int(sum(len(lb) for lb in labels)),
+            "protocol": "pseudo-GT = CPU oracle detections at conf .25; val NMS conf .001 multi-label iou .7"}
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without an external launcher: run this script under torch.distributed.run as a
+    CHILD process (one rank per GPU) and return its exit code.  The parent never touches the GPU (only
+    `import torch`, which does not initialise HIP), so no GPU-holding process is ever replaced by exec.
+    Same role as the reference's DDP launcher, U/utils/dist.py:25-66 (there: a temp script + torchrun)."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this driver
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *argv]
+    return subprocess.call(cmd, env=env)
+
+
+def stub_step_factory(B: int, world: int, rank: int):
+    """--stub-cpu: the multi-rank plumbing of a step (gloo, CPU) without a GPU -- each rank fills its
+    fixed-shape det/count buffers and takes part in the one all-gather.  Used by tests/test_bench_launch.py."""
+    from ydbl.parallel import gather_detections
+
+    det = torch.full((B, 300, 6), float(rank))
+    cnt = torch.full((B,), rank + 1, dtype=torch.int32)
+
+    def step():
+        if world > 1:
+            d, c = gather_detections(det, cnt, B * world)
+            assert d.shape[0] == B * world and int(c[-1]) == world
+
+    return step
 
 
 def main():
@@ -146,14 +249,22 @@ def main():
     ap.add_argument("--fp8", action="store_true", help="e4m3 dense-conv operands (BASELINE config 5)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--stub-cpu", action="store_true", help="gloo/CPU plumbing check of the N-rank launch (no GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the launcher started {world} ranks")
+    if args.stub_cpu:
+        return stub_main(args, world, rank)
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        assert dist.get_world_size() == args.gpus
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -179,16 +290,35 @@ def main():
         if world > 1:  # the path's only exchange: one all-gather of the fixed-shape box buffers
             gather_detections(det, cnt, B * world)
 
+    el = timed_steps(step, args, world, lambda: torch.cuda.synchronize(dev), dev)
+    extra = {"dets_per_image": round(float(sess.count.float().mean().item()), 2),
+             "candidates_per_image": round(float(sess.cand_count.float().mean().item()), 1),
+             "candidates_max": int(sess.cand_count.max().item())}
+    rf = None
+    if rank == 0 and not args.no_roofline:
+        rf = roofline(sess, dtype_name)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.model, S, B, gpu_session=(model, args.fp8))
+    if rank == 0:
+        emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def timed_steps(step, args, world, sync, dev=None) -> float:
+    """W untimed warmup steps, then exactly K steps bracketed by barrier + device sync on both sides;
+    returns the MAX over ranks of the timed wall clock (seconds)."""
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize(dev)
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize(dev)
+    sync()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -196,43 +326,43 @@ def main():
         t = torch.tensor([el], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = t.item()
-    images = B * world * args.steps
-    value = images / el
-    dets_per_img = float(sess.count.float().mean().item())
-    cands_per_img = float(sess.cand_count.float().mean().item())
-    cands_max = int(sess.cand_count.max().item())
+    return el
 
-    rf = None
-    if rank == 0 and not args.no_roofline:
-        rf = roofline(sess, dtype_name)
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.model, S)
+
+def emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu):
+    B, S = args.batch, args.imgsz
+    out = {
+        "metric": "images/sec @640×640 bs=32 (1/2/4/8 GPU) + mAP@0.5 vs CPU ref",
+        "value": round(B * world * args.steps / el, 2),
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(el * 1e3 / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype_name,
+        "data": "synthetic (blob images, trained-like synthetic weights tests/golden)",
+        "config": {"workload": f"YOLO-DBL-{args.model} {S}x{S} bs={B}/GPU {dtype_name} forward+decode+NMS "
+                               f"(conf .25, iou .7, max_det 300)" + (", RCCL all-gather of boxes" if world > 1 else ""),
+                   "model": Path(cfg).stem, "global_batch": B * world, "imgsz": S, "nc": 3,
+                   "parallelism": f"dp{world}"},
+        **extra,
+        "roofline": rf,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+
+
+def stub_main(args, world, rank):
+    if world > 1:
+        dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
+    step = stub_step_factory(args.batch, world, rank)
+    el = timed_steps(step, args, world, lambda: None)
     if rank == 0:
-        out = {
-            "metric": "images/sec @640×640 bs=32 (1/2/4/8 GPU) + mAP@0.5 vs CPU ref",
-            "value": round(value, 2),
-            "unit": "images/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(el * 1e3 / args.steps, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": dtype_name,
-            "data": "synthetic (blob images, trained-like synthetic weights tests/golden)",
-            "config": {"workload": f"YOLO-DBL-{args.model} {S}x{S} bs={B}/GPU {dtype_name} forward+decode+NMS "
-                                   f"(conf .25, iou .7, max_det 300)" + (", RCCL all-gather of boxes" if world > 1 else ""),
-                       "model": Path(cfg).stem, "global_batch": B * world, "imgsz": S, "nc": 3,
-                       "parallelism": f"dp{world}"},
-            "dets_per_image": round(dets_per_img, 2),
-            "candidates_per_image": round(cands_per_img, 1),
-            "candidates_max": cands_max,
-            "roofline": rf,
-            "cpu_baseline": cpu,
-        }
-        print(json.dumps(out))
+        emit_line(args, world, el, "stub", CFGS[args.model][0], {"stub": "gloo/CPU plumbing, no GPU work"}, None, None)
     if world > 1:
         dist.destroy_process_group()
 

@@ -95,3 +95,19 @@ def test_checkpoint_refuses_foreign_globals(tmp_path):
     torch.save({"ema": Payload()}, path)
     with pytest.raises(RuntimeError, match="outside the allowed"):
         read_reference_checkpoint(path)
+
+
+def test_partial_state_dict_is_refused():
+    """A dict that covers only part of the model must not load silently (layers would stay at random
+    init); BN's num_batches_tracked counters may be absent (they carry no weight)."""
+    from ydbl import YOLO
+
+    m = YOLO("yolov13n_DBL.yaml", nc=3)
+    sd = m.model.state_dict()
+    partial = {k: v for i, (k, v) in enumerate(sd.items()) if i % 7}
+    with pytest.raises(KeyError, match="missing"):
+        YOLO("yolov13n_DBL.yaml", nc=3).load(partial)
+    no_counters = {k: v for k, v in sd.items() if not k.endswith("num_batches_tracked")}
+    YOLO("yolov13n_DBL.yaml", nc=3).load(no_counters)
+    with pytest.raises(KeyError, match="unexpected"):
+        YOLO("yolov13n_DBL.yaml", nc=3).load({**sd, "model.99.bogus": torch.zeros(1)})

@@ -191,3 +191,23 @@ def test_map50_gpu_vs_cpu_pseudo_gt(golden_dir, half):
         return
     assert abs(m_gpu - m_cpu) <= 0.1
     assert m_cpu > 0.5
+
+
+def test_checkpoint_predict_matches_state_dict(tmp_path, golden_dir):
+    """YOLO('best.pt') on a reference-format checkpoint (fp16 EMA pickled under the reference's class
+    paths, U/engine/trainer.py:513-546) predicts exactly what the same weights loaded as a state_dict do."""
+    from test_checkpoint import _save_reference_style
+    from ydbl import YOLO
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    path = tmp_path / "best.pt"
+    _save_reference_style(p.model, path)
+    sd = {k: v.half().float() if v.is_floating_point() else v for k, v in p.model.state_dict().items()}
+    a = YOLO(path)
+    b = YOLO("yolov13n_DBL.yaml", nc=3).load(sd)
+    x = blob_images(2, 256, seed=3)
+    ra, rb = a.predict(x, conf=0.05, half=True), b.predict(x, conf=0.05, half=True)
+    assert sum(len(r.boxes.data) for r in ra) > 0
+    for u, v in zip(ra, rb):
+        assert torch.equal(u.boxes.data, v.boxes.data)

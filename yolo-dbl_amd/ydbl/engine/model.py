@@ -121,6 +121,11 @@ class Model:
         missing, unexpected = self.model.load_state_dict(sd, strict=False)
         if unexpected:
             raise KeyError(f"unexpected keys in weights: {unexpected[:5]} ...")
+        # BN's num_batches_tracked counter carries no weight (the reference's checkpoints may omit it);
+        # every other parameter/buffer must be present: a partial dict would leave layers at random init
+        missing = [k for k in missing if not k.endswith("num_batches_tracked")]
+        if missing:
+            raise KeyError(f"{len(missing)} keys missing from weights: {missing[:5]} ...")
         self._sessions.clear()
 
     def state_dict(self):

@@ -129,10 +129,21 @@ class Plan:
         return w is not None and w[0] < step
 
     def fuse_second_output(self, writer, y2: TV, r2: TV, a2: float, b2: float) -> TV | None:
-        """Give the conv launch `writer` the second output y2 = a2 * y + b2 * r2; None if it has one."""
+        """Give the conv / DySample launch `writer` the second output y2 = a2 * y + b2 * r2.  None (the
+        caller then emits a separate ydbl_gate_add) when it already has one or when y2 / r2 break the
+        launch-time rules of that entry point: same shape and dtype as y, channel stride % 4 for the
+        conv epilogue (ydbl_conv2d_nhwc), 16-byte vectors and pointers for ydbl_dysample_ex."""
         _, d = writer
         if d.y2.ptr:
             return None
+        y = d.y
+        for v in (y2, r2):
+            if (v.n, v.h, v.w, v.c) != (y.n, y.h, y.w, y.c) or _lib.dtype_code(v.dtype) != y.dtype or v.cs % 4:
+                return None
+            if isinstance(d, _lib.DySampleDesc):
+                vec = 16 // v.base.element_size()
+                if v.cs % vec or v.c % vec or v.ptr % 16:
+                    return None
         d.y2, d.r2, d.a2, d.b2 = y2.struct(), r2.struct(), float(a2), float(b2)
         self.steps[writer[0]].keep.append((y2, r2))
         return y2
