@@ -52,19 +52,19 @@ def conv_traffic(step, elsize):
 
 def roofline(session, dtype_name, reps=3):
     """Per-launch HIP-event timing of one eager forward; dominant kernel = the dense conv."""
-    plan = session.plan
     elsize = 4 if dtype_name == "fp32" else 2  # activation bytes (fp8 mode keeps fp16 activations)
-    best = None
-    for _ in range(reps):
-        t = plan.run_timed()
-        if best is None:
-            best = t
-        else:
-            best = [(w, min(a, b)) for (w, a), (_, b) in zip(best, t)]
+    steps, best = [], []
+    for plan in session.plans:  # one plan per sub-batch stream (each launch timed on its own)
+        bp = None
+        for _ in range(reps):
+            t = plan.run_timed()
+            bp = t if bp is None else [(w, min(a, b)) for (w, a), (_, b) in zip(bp, t)]
+        steps += plan.steps
+        best += bp
     conv_ms = conv_bytes = conv_flops = 0.0
     by_kind = {}
     n_conv = 0
-    for st, (what, ms) in zip(plan.steps, best):
+    for st, (what, ms) in zip(steps, best):
         kind = st.fn.__name__
         by_kind[kind] = by_kind.get(kind, 0.0) + ms
         if kind == "ydbl_conv2d_nhwc":
@@ -247,6 +247,8 @@ def main():
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--fp32", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="e4m3 dense-conv operands (BASELINE config 5)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-batch graphs replayed concurrently on this many HIP streams (DetectSession)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stub-cpu", action="store_true", help="gloo/CPU plumbing check of the N-rank launch (no GPU)")
@@ -278,7 +280,8 @@ def main():
     model = YOLO(cfg, nc=3)
     load_trained(model.model, ROOT / "tests" / "golden" / fx)
     B, S = args.batch, args.imgsz
-    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=args.fp8)
+    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=args.fp8,
+                         streams=args.streams)
     if args.fp8:  # activation scales from a separate synthetic calibration batch
         sess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
     # synthetic images, different per rank, resident in the session's input buffer (HBM)
@@ -347,7 +350,7 @@ def emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu):
         "config": {"workload": f"YOLO-DBL-{args.model} {S}x{S} bs={B}/GPU {dtype_name} forward+decode+NMS "
                                f"(conf .25, iou .7, max_det 300)" + (", RCCL all-gather of boxes" if world > 1 else ""),
                    "model": Path(cfg).stem, "global_batch": B * world, "imgsz": S, "nc": 3,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "streams_per_gpu": args.streams},
         **extra,
         "roofline": rf,
         "cpu_baseline": cpu,

@@ -184,10 +184,11 @@ def match_detections(ref, got, y_ref, conf, iou, tol_box, tol_conf, max_det=300)
     return out
 
 
-def gpu_pred(p, x, half=False, fp8=False, conf=0.25, iou=0.7, calib=None):
+def gpu_pred(p, x, half=False, fp8=False, conf=0.25, iou=0.7, calib=None, streams=1):
     """Decoded predictions + final detections of the product path (HIP through libydbl)."""
     B, _, H, W = x.shape
-    s = p.session(B, H, W, half=half, conf=conf, iou=iou, keep_pred=True, use_graph=False, fp8=fp8)
+    s = p.session(B, H, W, half=half, conf=conf, iou=iou, keep_pred=True, use_graph=streams > 1, fp8=fp8,
+                  streams=streams)
     if fp8:
         s.calibrate_fp8((calib if calib is not None else x).cuda())
     s(x.cuda())

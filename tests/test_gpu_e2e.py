@@ -45,7 +45,7 @@ def _product(scale, golden_dir):
     return _PRODUCT[scale]
 
 
-def _run(golden_dir, name, batch, mode):
+def _run(golden_dir, name, batch, mode, streams=1):
     from ydbl.utils.synthetic import blob_images
 
     y64, meta = load_e2e(golden_dir, name)
@@ -56,7 +56,7 @@ def _run(golden_dir, name, batch, mode):
     p = _product(meta["scale"], golden_dir)
     calib = blob_images(batch, S, seed=4321) if mode == "fp8" else None
     yg, dets = gpu_pred(p, x, half=mode != "fp32", fp8=mode == "fp8", conf=meta["conf"], iou=meta["iou"],
-                        calib=calib)
+                        calib=calib, streams=streams)
     yg = yg[ref]
     dets = [dets[i] for i in ref]
     ref_dets = detections(y64, meta["conf"], meta["iou"], (S, S))
@@ -81,9 +81,11 @@ def test_e2e_fp32(golden_dir, name, batch):
     assert m["borderline"] == 0 and m["pairs"] == sum(len(d) for d in ref_dets), m
 
 
-@pytest.mark.parametrize("name,batch", [("n640", 32), ("n640", 2), ("s640", 8), ("s640", 32), ("l1280", 8)])
-def test_e2e_fp16(golden_dir, name, batch):
-    y64, meta, yg, dets, ref_dets = _run(golden_dir, name, batch, "fp16")
+@pytest.mark.parametrize("name,batch,streams", [("n640", 32, 1), ("n640", 32, 2), ("n640", 2, 1), ("s640", 8, 1),
+                                                ("s640", 32, 2), ("l1280", 8, 1)])
+def test_e2e_fp16(golden_dir, name, batch, streams):
+    """streams=2: the bench's layout (two bs/2 sub-batch graphs replayed on two HIP streams)."""
+    y64, meta, yg, dets, ref_dets = _run(golden_dir, name, batch, "fp16", streams)
     o16 = meta["oracle_fp16"]
     st = err_stats(yg, y64)
     tb, tc = fp16_rule(o16)

@@ -211,3 +211,27 @@ def test_checkpoint_predict_matches_state_dict(tmp_path, golden_dir):
     assert sum(len(r.boxes.data) for r in ra) > 0
     for u, v in zip(ra, rb):
         assert torch.equal(u.boxes.data, v.boxes.data)
+
+
+def test_split_session_equals_separate_sessions(golden_dir):
+    """streams=2 (two sub-batch graphs on two HIP streams writing slices of shared outputs) == the two
+    sub-batches run as separate single-stream sessions, bit for bit (same kernels at the same sizes)."""
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    x = blob_images(6, 192, seed=21).cuda()
+    split = p.session(6, 192, 192, half=True, conf=0.05, keep_pred=True, streams=2)
+    assert len(split.children) == 2 and [c.batch for c in split.children] == [3, 3]
+    for _ in range(2):
+        d, c = split(x)
+    torch.cuda.synchronize()
+    d, c, pred = d.clone(), c.clone(), split.pred.clone()
+    for i, (a, b) in enumerate(split.bounds):
+        one = p.session(b - a, 192, 192, half=True, conf=0.05, keep_pred=True)
+        d1, c1 = one(x[a:b])
+        torch.cuda.synchronize()
+        assert torch.equal(c1, c[a:b]) and torch.equal(one.pred, pred[a:b])
+        for j in range(b - a):  # rows past count[j] are not written (fixed-shape output buffer)
+            n = int(c1[j])
+            assert torch.equal(d1[j, :n], d[a + j, :n])
+    assert sum(len(r) for r in split.results()) > 0

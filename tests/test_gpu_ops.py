@@ -81,6 +81,52 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
 
 
+@pytest.mark.parametrize("cin,cout,n,h,w,res,second", [
+    (128, 64, 32, 40, 40, None, False),    # DBL-n neck 1x1s at bs 32: two 16-px tiles per wave
+    (64, 128, 32, 40, 40, "add", True),    # Cout 128: 128-wide column; residual + FullPAD second output
+    (256, 128, 32, 20, 20, None, False),   # K 256 (8 k-steps), 64-wide columns
+    (128, 256, 32, 20, 20, "mul", False),  # LSK.conv shape (residual multiply), 2 columns
+    (128, 32, 3, 17, 19, None, True),      # DySample.offset-like Cout 32, ragged pixel count
+    (96, 80, 2, 9, 13, None, False),       # K 96 (3 k-steps), Cout 80: tail column
+    (192, 3, 1, 7, 9, None, False),        # Cout 3 (Detect cls width), K 192
+    (32, 16, 4, 33, 5, "add", False),      # K 32, one k-step
+])
+def test_conv1x1_one_shot(cin, cout, n, h, w, res, second):
+    """fp16 pointwise convs with K <= 256 take conv1x1.hip (all loads of a workgroup in one round
+    trip): vs F.conv2d fp32 on the fp16-rounded operands, input/output as channel slices."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + 7 * cout + h)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 1, 1) / cin ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.half().float(), wt.half().float(), b))
+    plan = _plan(torch.float16)
+    xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+    ybuf = plan.alloc(n, h, w, cout + 16)
+    yv = ybuf.cslice(8, cout)
+    rv, mode = None, _lib.RES_NONE
+    if res:
+        r = torch.randn(n, cout, h, w)
+        rv = _tv_from_nchw(plan, r)
+        mode = _lib.RES_ADD if res == "add" else _lib.RES_MUL
+        r = r.half().float()
+        ref = r + ref if res == "add" else r * ref
+    emit_dense(plan, xv, yv, wt, b, 1, 0, 1, _lib.ACT_SILU, rv, mode)
+    if second:  # fused FullPAD: y2 = 0.5 * y + r2
+        r2 = torch.randn(n, cout, h, w)
+        r2v = _tv_from_nchw(plan, r2)
+        y2 = plan.alloc(n, h, w, cout)
+        assert plan.fuse_second_output(plan.writer_of(yv), y2, r2v, 0.5, 1.0) is not None
+    _run(plan)
+    got = yv.nchw().float().cpu()
+    torch.testing.assert_close(got, ref, rtol=2e-2, atol=2e-2)
+    if second:
+        want = 0.5 * got + r2.half().float()
+        torch.testing.assert_close(y2.nchw().float().cpu(), want, rtol=2e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("cin,cout,s,h,w,res", [
     (8, 8, 1, 70, 66, None), (8, 16, 2, 130, 140, None), (16, 8, 1, 67, 75, None), (16, 32, 2, 131, 129, "add"),
@@ -725,6 +771,47 @@ def test_dsconv_fused(dtype, cin, cout, k, s, shape):
     plan = _plan(dtype)
     assert M.fused_dsconv_ok(p_mod.dw, _tv_from_nchw(plan, x), dtype)
     _module_parity(o, p_mod, [x], dtype, tol)
+
+
+@pytest.mark.parametrize("n,h,w,add,sliced", [(32, 40, 40, True, True), (3, 13, 21, True, False), (1, 8, 8, False, False),
+                                              (2, 5, 3, True, True), (2, 20, 20, False, True)])
+def test_dsbottleneck_fused(n, h, w, add, sliced):
+    """ydbl_dsbottleneck_nhwc (cv1 -> cv2 of DSBottleneck with t on the CU, U/nn/modules/block.py:1408-1444)
+    == the two ydbl_dsconv_nhwc launches it replaces, bit for bit, and close to the oracle (fp16)."""
+    import os
+
+    from oracle import model as om
+    from ydbl.nn import modules as M
+    from ydbl.utils.synthetic import trained_like_
+
+    torch.manual_seed(n * 100 + h)
+    o = trained_like_(om.DSBottleneck(64, 64, shortcut=add, e=1.0, k1=3, k2=7), seed=h).eval()
+    x = torch.randn(n, 64, h, w)
+    outs = []
+    for fused in (True, False):
+        pm = M.DSBottleneck(64, 64, shortcut=add, e=1.0, k1=3, k2=7)
+        pm.load_state_dict(o.state_dict())
+        plan = _plan(torch.float16)
+        xv = _tv_from_nchw(plan, x, cs_extra=8 if sliced else 0, c_off=8 if sliced else 0)
+        ybuf = plan.alloc(n, h, w, 64 + (16 if sliced else 0))
+        yv = ybuf.cslice(8, 64) if sliced else ybuf
+        if fused:
+            os.environ["YDBL_DSBNECK"] = "1"
+        try:
+            pm.emit(plan, xv, yv)
+        finally:
+            os.environ.pop("YDBL_DSBNECK", None)
+        kinds = [st.fn.__name__ for st in plan.steps]
+        assert kinds == (["ydbl_dsbottleneck_nhwc"] if fused else ["ydbl_dsconv_nhwc"] * 2), kinds
+        _run(plan)
+        outs.append(yv.nchw().float().cpu())
+    with torch.no_grad():
+        ref = o(x)
+    d = (outs[0] - outs[1]).abs()
+    print(f"fused vs two launches: max {d.max().item():.3g}, {int((d > 0).sum())} of {d.numel()} differ; "
+          f"vs oracle: fused {(outs[0] - ref).abs().max().item():.3g}, two {(outs[1] - ref).abs().max().item():.3g}")
+    assert torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])

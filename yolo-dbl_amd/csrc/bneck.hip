@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     }
     h4 o;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = (_Float16)(inside ? silu_fast(acc[q] + bias1[q]) : 0.f);
+    for (int q = 0; q < 4; ++q) o[q] = f16_rne(inside ? silu_fast(acc[q] + bias1[q]) : 0.f);
     *reinterpret_cast<h4*>(mid_w + (vr * MP + vc) * 16) = o;
   };
   constexpr int WPT1 = 4 / NT1;
@@ -249,7 +249,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     if constexpr (PW) {  // cv2 output, rounded to fp16 as the unfused path stores it, -> LDS for the 1x1
       h4 o;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = (_Float16)v[q];
+      for (int q = 0; q < 4; ++q) o[q] = f16_rne(v[q]);
       *reinterpret_cast<h4*>(s_in + ((c2 >> 3) * (TH * 16) + j * 16 + r16) * 16 + (c2 & 7) * 2) = o;
     } else {
       store_f<4>(y.at(img, oy, ox) + c2, v);

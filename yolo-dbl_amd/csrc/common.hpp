@@ -110,21 +110,41 @@ __device__ __forceinline__ void load_f(const float* p, float* o) {
     for (int i = 0; i < N; ++i) o[i] = p[i];
   }
 }
+// fp32 -> fp16 as its own rounding step (round-to-nearest-even of the fp32 value).  hipcc otherwise
+// folds the op that produced the fp32 value (a multiply, an fmaf) into v_fma_mixlo_f16, which
+// rounds the EXACT result once to fp16: in rare near-tie cases 1 ulp away from the fp32 result
+// rounded to fp16 (the reference's accumulate-in-fp32-then-store), and chosen differently per
+// kernel, so two launch plans of the same arithmetic would not agree bit for bit.  The empty asm
+// pins the fp32 value in a VGPR.
+__device__ __forceinline__ _Float16 f16_rne(float v) {
+  asm volatile("" : "+v"(v));
+  return (_Float16)v;
+}
+__device__ __forceinline__ h4 to_h4_rne(const float* a) {
+  float v0 = a[0], v1 = a[1], v2 = a[2], v3 = a[3];
+  asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+  return h4{(_Float16)v0, (_Float16)v1, (_Float16)v2, (_Float16)v3};
+}
+
+// v as a stored T would hold it, back in fp32 (T = _Float16: f16_rne; T = float: v)
+template <typename T>
+__device__ __forceinline__ float round_to(float v) {
+  if constexpr (std::is_same<T, float>::value) return v;
+  else return float(f16_rne(v));
+}
+
 template <int N>
 __device__ __forceinline__ void store_f(_Float16* p, const float* v) {
   if constexpr (N == 8) {
     h8 o;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[i] = (_Float16)v[i];
+    for (int i = 0; i < 8; ++i) o[i] = f16_rne(v[i]);
     *reinterpret_cast<h8*>(p) = o;
   } else if constexpr (N == 4) {
-    h4 o;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[i] = (_Float16)v[i];
-    *reinterpret_cast<h4*>(p) = o;
+    *reinterpret_cast<h4*>(p) = to_h4_rne(v);
   } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i) p[i] = (_Float16)v[i];
+    for (int i = 0; i < N; ++i) p[i] = f16_rne(v[i]);
   }
 }
 template <int N>

@@ -157,7 +157,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
       if (co[i] + 4 <= p.Cout) {
         store_f<4>(yp, v);
       } else {
-        for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) yp[q] = (T)v[q];
+        for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) store_f<1>(yp + q, v + q);
       }
       if (p.y2) {  // uniform
         const T* r2p = p.r2 + pc * p.r2cs + co[i];
@@ -166,10 +166,15 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
           float r2v[4];
           load_f<4>(r2p, r2v);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) r2v[q] = p.a2 * float(T(v[q])) + p.b2 * r2v[q];
+          for (int q = 0; q < 4; ++q) {
+            r2v[q] = p.a2 * round_to<T>(v[q]) + p.b2 * r2v[q];  // y as stored (rounded to T)
+          }
           store_f<4>(y2p, r2v);
         } else {
-          for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) y2p[q] = T(p.a2 * float(T(v[q])) + p.b2 * float(r2p[q]));
+          for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) {
+            const float o = p.a2 * round_to<T>(v[q]) + p.b2 * float(r2p[q]);
+            store_f<1>(y2p + q, &o);
+          }
         }
       }
     }

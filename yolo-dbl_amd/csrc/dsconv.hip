@@ -25,9 +25,7 @@ __device__ __forceinline__ int bswz(int row, int kv) {  // B-tile slot: 16 conse
 }
 
 // 4 consecutive activation-dtype channels from 4 fp32 values (8 B f16 / 16 B f32).
-__device__ __forceinline__ void store4(_Float16* d, const float* a) {
-  *reinterpret_cast<h4*>(d) = h4{(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3]};
-}
+__device__ __forceinline__ void store4(_Float16* d, const float* a) { *reinterpret_cast<h4*>(d) = to_h4_rne(a); }
 __device__ __forceinline__ void store4(float* d, const float* a) {
   *reinterpret_cast<f32x4*>(d) = f32x4{a[0], a[1], a[2], a[3]};
 }

@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
   const float* xb = x + (int64_t)b * 3 * plane;
   auto pack = [&](float c0, float c1, float c2) {
     rec r;
-    r[0] = T(c0 * scale); r[1] = T(c1 * scale); r[2] = T(c2 * scale); r[3] = T(0.f);
+    r[0] = T(round_to<T>(c0 * scale)); r[1] = T(round_to<T>(c1 * scale)); r[2] = T(round_to<T>(c2 * scale)); r[3] = T(0.f);
     return r;
   };
   if constexpr (V4) {

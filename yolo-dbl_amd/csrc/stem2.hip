@@ -133,8 +133,8 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
       for (int e = 0; e < 4; ++e) {
         const int col = 4 * k - 2 + e;
         if (col < 0 || col >= Cfg::INW) continue;
-        in[r * Cfg::INW + col] = h4{(_Float16)(v[u][0][e] * scale), (_Float16)(v[u][1][e] * scale),
-                                    (_Float16)(v[u][2][e] * scale), (_Float16)0.f};
+        in[r * Cfg::INW + col] = h4{f16_rne(v[u][0][e] * scale), f16_rne(v[u][1][e] * scale),
+                                    f16_rne(v[u][2][e] * scale), (_Float16)0.f};
       }
     }
   } else {
@@ -144,9 +144,9 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
       h4 rec = h4{0, 0, 0, 0};
       if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
         const int64_t o = (int64_t)iy * W + ix;
-        rec[0] = (_Float16)(xb[o] * scale);
-        rec[1] = (_Float16)(xb[plane + o] * scale);
-        rec[2] = (_Float16)(xb[2 * plane + o] * scale);
+        rec[0] = f16_rne(xb[o] * scale);
+        rec[1] = f16_rne(xb[plane + o] * scale);
+        rec[2] = f16_rne(xb[2 * plane + o] * scale);
       }
       in[t] = rec;
     }
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const float sv = silu_fast(acc[q] + bias0[q]);
-      v[q] = (_Float16)(inside ? sv : 0.f);
+      v[q] = f16_rne(inside ? sv : 0.f);
     }
     const int rec = lr * 2 * Cfg::L0P + (lc & 1) * Cfg::L0P + (lc >> 1);
     *reinterpret_cast<h4*>(l0w + rec * 16) = v;

@@ -149,17 +149,21 @@ class Model:
 
     # ------------------------------------------------------------------ inference
     def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
-                multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True) -> DetectSession:
+                multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True,
+                streams=1) -> DetectSession:
+        """A compiled (batch, h, w, dtype, NMS settings) inference session; streams > 1 splits the batch into
+        that many concurrently replayed sub-batch graphs (DetectSession)."""
         dev = select_device(device)
         dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
-               bool(fp8), bool(clip))
+               bool(fp8), bool(clip), int(streams))
         s = self._sessions.get(key)
         if s is None:
             with torch.cuda.device(dev):
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
-                                  keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip)
+                                  keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip,
+                                  streams=streams)
             self._sessions[key] = s
         return s
 

@@ -19,14 +19,25 @@ from ..runtime import GraphRunner, Plan
 
 
 class DetectSession:
+    """streams = k > 1: the batch is split into k contiguous sub-batches, each compiled into its own launch
+    plan (own buffers, own hipGraph) and replayed on its own HIP stream, writing into slices of the shared
+    det / count (/ pred) outputs.  At DBL-n/s sizes every launch is short and ramp/tail-bound, so two
+    concurrent half-batch graphs fill each other's gaps (scripts/stream_probe.py: DBL-n bs32 +10 %,
+    DBL-s bs64 +14 %)."""
+
     def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
                  multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
-                 keep_pred=False, use_graph=True, device="cuda", fp8=False):
+                 keep_pred=False, use_graph=True, device="cuda", fp8=False, streams=1, _outputs=None):
         if fp8 and dtype != torch.float16:
             raise ValueError("fp8 operands run on the fp16 activation path (half=True)")
         self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
         self.fp8, self.fp8_ready = bool(fp8), False
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
+        self.children = []
+        if streams > 1 and batch >= streams:
+            self._init_split(model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes, max_nms,
+                             max_wh, clip, keep_pred, use_graph, device, fp8, streams)
+            return
         cm = model.compile(batch, h, w, dtype, device=device)
         self.compiled = cm
         plan: Plan = cm.plan
@@ -42,9 +53,12 @@ class DetectSession:
         self.cand_cls = torch.empty((batch, cap), dtype=torch.int32, device=dev)
         self.cand_idx = torch.empty((batch, cap), dtype=torch.int32, device=dev)
         self.cand_count = torch.zeros((batch,), dtype=torch.int32, device=dev)
-        self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
-        self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
-        self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+        if _outputs is not None:  # slices of a split session's shared outputs
+            self.det, self.count, self.pred = _outputs
+        else:
+            self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
+            self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
+            self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
         self.classes_t = (torch.tensor(list(classes), dtype=torch.int32, device=dev) if classes is not None else None)
         ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(batch, cap, max_nms)), dtype=torch.uint8, device=dev)
         plan.buffers += [self.cand_box, self.cand_score, self.cand_cls, self.cand_idx, self.cand_count, self.det,
@@ -65,12 +79,52 @@ class DetectSession:
                      float(h) if clip else 0.0, self.det.data_ptr(), self.count.data_ptr(), ws.data_ptr())
         plan.launch("ydbl_nms", nd, what="NMS", keep=[nd])
         self.plan = plan
+        self.plans = [plan]
         self.use_graph = use_graph
         self._graph = None
+
+    def _init_split(self, model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes, max_nms,
+                    max_wh, clip, keep_pred, use_graph, device, fp8, streams):
+        from ..parallel import shard_bounds
+
+        dev = torch.device(device)
+        det = model.model[-1]
+        nc = det.nc
+        A = sum((h // int(s)) * (w // int(s)) for s in det.stride.tolist())
+        self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
+        self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+        self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
+        self.bounds = [shard_bounds(batch, streams, r) for r in range(streams)]
+        for a, b in self.bounds:
+            outs = (self.det[a:b], self.count[a:b], self.pred[a:b] if keep_pred else None)
+            self.children.append(DetectSession(model, b - a, h, w, dtype, conf, iou, max_det, multi_label, agnostic,
+                                               classes, max_nms, max_wh, clip, keep_pred, use_graph, device, fp8,
+                                               _outputs=outs))
+        self.streams = [torch.cuda.Stream(dev) for _ in self.children]
+        self.plans = [c.plan for c in self.children]
+        self.plan = self.plans[0]
+        self.use_graph = use_graph
+        self.nc, self.A = self.children[0].nc, self.children[0].A
+
+    @property
+    def cand_count(self):
+        if self.children:
+            return torch.cat([c.cand_count for c in self.children])
+        return self._cand_count
+
+    @cand_count.setter
+    def cand_count(self, v):
+        self._cand_count = v
 
     # ------------------------------------------------------------------ execution
     def load(self, x: torch.Tensor):
         """Copy a BCHW float batch into the static input buffer (LoadTensor semantics are the caller's)."""
+        if self.children:
+            if tuple(x.shape[1:]) != (3, self.h, self.w) or x.shape[0] != self.batch:
+                raise ValueError(f"input shape {tuple(x.shape)} != session shape {(self.batch, 3, self.h, self.w)}")
+            for c, (a, b) in zip(self.children, self.bounds):
+                c.load(x[a:b])
+            return
         if tuple(x.shape) != tuple(self.compiled.input.shape):
             raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
         self.compiled.input.copy_(x, non_blocking=True)
@@ -82,6 +136,10 @@ class DetectSession:
 
         if x is not None:
             self.load(x)
+        if self.children:
+            n = sum(c.calibrate_fp8() for c in self.children)
+            self.fp8_ready = True
+            return n
         n = enable_fp8(self.plan, self.plan.run)
         self._graph = None  # descriptors changed: recapture
         self.fp8_ready = True
@@ -90,6 +148,15 @@ class DetectSession:
     def launch(self):
         if self.fp8 and not self.fp8_ready:
             self.calibrate_fp8()  # first batch calibrates (dynamic post-training quantization)
+        if self.children:  # fork: each sub-batch's graph on its own stream, then join
+            cur = torch.cuda.current_stream(self.det.device)
+            for c, st in zip(self.children, self.streams):
+                st.wait_stream(cur)
+                with torch.cuda.stream(st):
+                    c.launch()
+            for st in self.streams:
+                cur.wait_stream(st)
+            return
         if self.use_graph:
             if self._graph is None:
                 self._graph = GraphRunner(self.plan)
@@ -110,4 +177,6 @@ class DetectSession:
         return [det[i, : cnt[i]].clone() for i in range(self.batch)]
 
     def feats(self):
+        if self.children:
+            raise RuntimeError("feats() of a split (streams > 1) session: use streams=1")
         return self.compiled.feats()
