@@ -247,7 +247,7 @@ def main():
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--fp32", action="store_true")
     ap.add_argument("--fp8", action="store_true", help="e4m3 dense-conv operands (BASELINE config 5)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=1,
                     help="sub-batch graphs replayed concurrently on this many HIP streams (DetectSession)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")

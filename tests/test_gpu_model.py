@@ -231,7 +231,5 @@ def test_split_session_equals_separate_sessions(golden_dir):
         d1, c1 = one(x[a:b])
         torch.cuda.synchronize()
         assert torch.equal(c1, c[a:b]) and torch.equal(one.pred, pred[a:b])
-        for j in range(b - a):  # rows past count[j] are not written (fixed-shape output buffer)
-            n = int(c1[j])
-            assert torch.equal(d1[j, :n], d[a + j, :n])
+        assert torch.equal(d1, d[a:b])  # rows past count are zeroed by the NMS kernel
     assert sum(len(r) for r in split.results()) > 0

@@ -437,7 +437,18 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     dst[4] = p.cscore[o];
     dst[5] = float(p.ccls[o]);
   }
+  // rows kept..max_det of the fixed-shape output are zeroed (the all-gather ships whole buffers)
+  float* rest = p.out + ((int64_t)b * p.max_det + kept) * 6;
+  for (int k = threadIdx.x; k < (p.max_det - kept) * 6; k += NMS_THREADS) rest[k] = 0.f;
   if (threadIdx.x == 0) p.out_count[b] = kept;
+}
+
+// Zeroes the per-image candidate counters ahead of the decode's atomics.  A kernel, not
+// hipMemsetAsync: a memset captured into a hipGraph was observed (ROCm 7.x) NOT to be ordered before
+// the following kernel on some replays -- the counters then carried the previous replay's totals and
+// NMS saw stale candidates (tests/test_gpu_model.py::test_split_session_equals_separate_sessions).
+__global__ void zero_counts_kernel(int* c, int n) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) c[i] = 0;
 }
 
 static int next_pow2(int v) {
@@ -469,7 +480,7 @@ static int decode_t(const ydbl_decode_desc* d, hipStream_t s) {
   a.cbox = d->cand_box; a.cscore = d->cand_score; a.ccls = d->cand_cls; a.cidx = d->cand_idx; a.ccount = d->cand_count;
   a.cap = d->cap;
   const int B = d->box[0].n;
-  if (hipMemsetAsync(d->cand_count, 0, sizeof(int) * B, s) != hipSuccess) return check_launch("decode memset");
+  zero_counts_kernel<<<1, 256, 0, s>>>(d->cand_count, B);
   decode_kernel<T><<<dim3((unsigned)cdiv(A, 256), B), 256, 0, s>>>(a);
   return check_launch("ydbl_detect_decode");
 }
@@ -502,7 +513,7 @@ extern "C" int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream) 
   if (!d->cand_box || !d->cand_score || !d->cand_cls || !d->cand_idx || !d->cand_count || d->cap < 1)
     return fail(YDBL_EINVAL, "pred_candidates: null candidate buffers");
   hipStream_t s = as_stream(stream);
-  if (hipMemsetAsync(d->cand_count, 0, sizeof(int) * d->n, s) != hipSuccess) return check_launch("pred memset");
+  zero_counts_kernel<<<1, 256, 0, s>>>(d->cand_count, d->n);
   pred_cand_kernel<<<dim3((unsigned)cdiv(d->A, 256), d->n), 256, 0, s>>>(*d);
   return check_launch("ydbl_pred_candidates");
 }
