@@ -34,24 +34,81 @@ CFGS = {"n": ("yolov13n_DBL.yaml", "trained_yolov13n_DBL_nc3.npz"),
         "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc3.npz")}
 
 
+def _px(v):
+    return v.n * v.h * v.w
+
+
 def conv_traffic(step, elsize):
-    """Algorithmic bytes / FLOPs of one ydbl_conv2d_nhwc launch from its descriptor."""
+    """Algorithmic bytes / FLOPs of one ydbl_conv2d_nhwc launch from its descriptor: input read once,
+    output written once (+ residual read, + fused FullPAD second output and its other input), weights once."""
     d = step.args[0]
     x, y = d.x, d.y
     cin = x.c
     k = d.kh * d.kw
     wsize = 1 if d.dq else elsize  # e4m3 weights in fp8 mode
-    byts = (x.n * x.h * x.w * cin + y.n * y.h * y.w * y.c) * elsize + y.c * k * cin * wsize
+    byts = (_px(x) * cin + _px(y) * y.c) * elsize + y.c * k * cin * wsize
     if d.res_mode:
-        byts += y.n * y.h * y.w * y.c * elsize
-    if d.y2.ptr:  # fused FullPAD: second output written + its other input read
-        byts += 2 * y.n * y.h * y.w * y.c * elsize
-    flops = 2.0 * y.n * y.h * y.w * y.c * k * cin
-    return byts, flops
+        byts += _px(y) * y.c * elsize
+    if d.y2.ptr:
+        byts += 2 * _px(y) * y.c * elsize
+    return byts, 2.0 * _px(y) * y.c * k * cin
+
+
+def dsconv_traffic(step, elsize):
+    """ydbl_dsconv_nhwc: x read, y written (+ residual, + the fused class-conv output), dw + pw weights."""
+    d = step.args[0]
+    x, y = d.x, d.y
+    byts = (_px(x) * x.c + _px(y) * y.c) * elsize + x.c * d.k * d.k * 4 + y.c * x.c * elsize
+    if d.res_mode:
+        byts += _px(y) * y.c * elsize
+    if d.tail_w:
+        byts += _px(y) * d.tail_n * elsize
+    return byts, 2.0 * _px(y) * x.c * (d.k * d.k + y.c)
+
+
+def bneck_traffic(step, elsize):
+    """ydbl_bottleneck_nhwc: Conv3x3(c_in, c_mid) -> Conv3x3(c_mid, c) [-> 1x1 c -> c]: x read, y written."""
+    d = step.args[0]
+    x, y = d.x, d.y
+    cm = d.c_mid or d.c // 2
+    flops = 2.0 * _px(y) * (x.c * 9 * cm + cm * 9 * d.c + (d.c * d.c if d.pw else 0))
+    return (_px(x) * x.c + _px(y) * y.c) * elsize, flops
+
+
+def stem2_traffic(step, elsize):
+    """ydbl_conv_stem2: the fp32 NCHW image read, layer 1's output written (layer 0's stays on chip)."""
+    d = step.args[0]
+    c0 = d.c0
+    flops = 2.0 * d.n * d.h * d.w * c0 * 27 + 2.0 * _px(d.y) * 2 * c0 * 9 * c0
+    return d.n * d.cin * d.h * d.w * 4 + _px(d.y) * d.y.c * elsize, flops
+
+
+def dsbneck_traffic(step, elsize):
+    """ydbl_dsbottleneck_nhwc: x read (+ residual), y written; the intermediate stays on chip."""
+    d = step.args[0]
+    c = d.x.c
+    byts = (_px(d.x) * c * (2 if d.add else 1) + _px(d.y) * c) * elsize
+    return byts, 2.0 * _px(d.y) * c * (9 + c + 49 + c)
+
+
+def dysample_traffic(step, elsize):
+    """ydbl_dysample_ex: x + offsets read, the 2x-upsampled y written (+ fused FullPAD second output)."""
+    d = step.args[0]
+    byts = (_px(d.x) * d.x.c + _px(d.off) * d.off.c + _px(d.y) * d.y.c) * elsize
+    if d.y2.ptr:
+        byts += 2 * _px(d.y) * d.y.c * elsize
+    return byts, 0.0
+
+
+TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("dsconv", dsconv_traffic),
+           "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
+           "ydbl_dsbottleneck_nhwc": ("dsbottleneck", dsbneck_traffic),
+           "ydbl_dysample_ex": ("dysample", dysample_traffic)}
 
 
 def roofline(session, dtype_name, reps=3):
-    """Per-launch HIP-event timing of one eager forward; dominant kernel = the dense conv."""
+    """Per-launch HIP-event timing of one eager walk of every plan of the session (min of `reps`); the
+    dominant kernel family (most time) = the dense conv; a per-family table beside it."""
     elsize = 4 if dtype_name == "fp32" else 2  # activation bytes (fp8 mode keeps fp16 activations)
     steps, best = [], []
     for plan in session.plans:  # one plan per sub-batch stream (each launch timed on its own)
@@ -61,48 +118,74 @@ def roofline(session, dtype_name, reps=3):
             bp = t if bp is None else [(w, min(a, b)) for (w, a), (_, b) in zip(bp, t)]
         steps += plan.steps
         best += bp
-    conv_ms = conv_bytes = conv_flops = 0.0
-    by_kind = {}
-    n_conv = 0
+    by_kind, fam = {}, {}
     for st, (what, ms) in zip(steps, best):
         kind = st.fn.__name__
         by_kind[kind] = by_kind.get(kind, 0.0) + ms
-        if kind == "ydbl_conv2d_nhwc":
-            b, f = conv_traffic(st, elsize)
-            conv_ms += ms
-            conv_bytes += b
-            conv_flops += f
-            n_conv += 1
-    total_ms = sum(ms for _, ms in best)
-    ach_gbs = conv_bytes / (conv_ms * 1e-3) / 1e9
-    ach_tf = conv_flops / (conv_ms * 1e-3) / 1e12
-    ai = conv_flops / conv_bytes
-    ridge = MFMA_PEAK_TFLOPS[dtype_name] * 1e12 / (HBM_PEAK_GBS * 1e9)
-    bound = "hbm" if ai < ridge else "mfma"
-    if bound == "hbm":
+        if kind in TRAFFIC:
+            name, fn = TRAFFIC[kind]
+            b, f = fn(st, elsize)
+            e = fam.setdefault(name, {"launches": 0, "ms": 0.0, "bytes": 0.0, "flops": 0.0})
+            e["launches"] += 1
+            e["ms"] += ms
+            e["bytes"] += b
+            e["flops"] += f
+    pk = MFMA_PEAK_TFLOPS[dtype_name]
+    pmc = pmc_summary()
+    families = {}
+    for name, e in sorted(fam.items(), key=lambda kv: -kv[1]["ms"]):
+        gbs = e["bytes"] / (e["ms"] * 1e-3) / 1e9
+        tf = e["flops"] / (e["ms"] * 1e-3) / 1e12
+        families[name] = {"launches": e["launches"], "avg_launch_us": round(e["ms"] * 1e3 / e["launches"], 2),
+                          "alg_bytes_per_launch": int(e["bytes"] / e["launches"]), "GB_s": round(gbs, 1),
+                          "hbm_frac": round(gbs / HBM_PEAK_GBS, 4), "TFLOP_s": round(tf, 2),
+                          "mfma_frac": round(tf / pk, 4)}
+        if pmc and name in pmc["families"]:
+            pf = pmc["families"][name]
+            families[name]["pmc_hbm_bytes_per_launch"] = pf.get("hbm_bytes_per_launch")
+            families[name]["mfma_busy"] = pf.get("mfma_busy")
+    c = fam["conv2d"]
+    ach_gbs = c["bytes"] / (c["ms"] * 1e-3) / 1e9
+    ach_tf = c["flops"] / (c["ms"] * 1e-3) / 1e12
+    ai = c["flops"] / c["bytes"]
+    ridge = pk * 1e12 / (HBM_PEAK_GBS * 1e9)
+    if ai < ridge:
         rf = {"bound": "hbm", "achieved": round(ach_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
               "frac": round(ach_gbs / HBM_PEAK_GBS, 4)}
     else:
-        pk = MFMA_PEAK_TFLOPS[dtype_name]
         rf = {"bound": "mfma", "achieved": round(ach_tf, 2), "peak": pk, "unit": "TFLOP/s", "frac": round(ach_tf / pk, 4)}
-    rf.update({"kernel": "ydbl_conv2d_nhwc", "launches_per_step": n_conv,
-               "avg_launch_us": round(conv_ms * 1e3 / max(n_conv, 1), 2),
-               "alg_bytes_per_launch": int(conv_bytes / max(n_conv, 1)),
-               "alg_flops_per_step": conv_flops, "arith_intensity": round(ai, 1), "tflops": round(ach_tf, 2),
-               "eager_step_ms": round(total_ms, 3),
-               "ms_by_kernel": {k: round(v, 3) for k, v in sorted(by_kind.items(), key=lambda kv: -kv[1])}})
-    rf["traffic"] = pmc_traffic()
+    pc = pmc["families"].get("conv2d", {}) if pmc else {}
+    rf.update({"kernel": "ydbl_conv2d_nhwc", "launches_per_step": c["launches"],
+               "avg_launch_us": round(c["ms"] * 1e3 / c["launches"], 2),
+               "alg_bytes_per_launch": int(c["bytes"] / c["launches"]), "alg_flops_per_step": c["flops"],
+               "arith_intensity": round(ai, 1), "tflops": round(ach_tf, 2),
+               "eager_step_ms": round(sum(ms for _, ms in best), 3),
+               "ms_by_kernel": {k: round(v, 3) for k, v in sorted(by_kind.items(), key=lambda kv: -kv[1])},
+               "traffic": pc.get("hbm_bytes_per_launch"), "mfma_busy": pc.get("mfma_busy"),
+               "code_hash": code_hash(),
+               "pmc_summary": pmc["file"] if pmc else "none for this code hash (scripts/pmc_families.sh)",
+               "families": families})
     return rf
 
 
-def pmc_traffic():
-    """HBM bytes per conv launch from the committed rocprofv3 PMC summary (gfx950-corrected), if present."""
-    p = ROOT / "profiles" / "pmc_conv_summary.json"
-    if p.exists():
+def code_hash() -> str:
+    sys.path.insert(0, str(ROOT / "scripts"))
+    from pmc_summary import code_hash as ch
+
+    return ch()
+
+
+def pmc_summary():
+    """The newest committed profiles/*_pmc_families.json measured on THIS code (matching source hash)."""
+    h = code_hash()
+    for p in sorted((ROOT / "profiles").rglob("*_pmc_families.json"), reverse=True):
         try:
-            return json.loads(p.read_text()).get("hbm_bytes_per_launch")
+            d = json.loads(p.read_text())
         except Exception:
-            return None
+            continue
+        if d.get("code_hash") == h:
+            d["file"] = str(p.relative_to(ROOT))
+            return d
     return None
 
 

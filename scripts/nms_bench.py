@@ -1,4 +1,5 @@
-"""Time ydbl_pred_candidates + ydbl_nms on synthetic predictions with a controlled candidate count."""
+"""Time ydbl_nms alone (HIP events, 20 back-to-back launches) on synthetic candidates: bs 32 images
+with a controlled candidate count per image (plus one heavy image, like the bench's max)."""
 import sys
 from pathlib import Path
 
@@ -6,28 +7,50 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "yolo-dbl_amd"))
 import torch  # noqa: E402
 
-from ydbl.utils.ops import non_max_suppression  # noqa: E402
+from ydbl import _lib  # noqa: E402
+from ydbl._lib import NmsDesc, PredCandDesc  # noqa: E402
 
 
-def pred(B, nc, A, frac, seed=0):
+def pred(B, nc, A, counts, seed=0):
     g = torch.Generator().manual_seed(seed)
     xy = torch.rand(B, 2, A, generator=g) * 600 + 20
     wh = torch.rand(B, 2, A, generator=g) * 80 + 4
     sc = torch.rand(B, nc, A, generator=g) * 0.2
-    k = int(frac * A)
-    sc[:, 0, :k] = 0.3 + 0.7 * torch.rand(B, k, generator=g)
+    for b, k in enumerate(counts):
+        sc[b, 0, :k] = 0.3 + 0.7 * torch.rand(k, generator=g)
     return torch.cat([xy, wh, sc], 1).cuda()
 
 
-for n_cand in (0, 50, 400, 2000, 8000):
-    p = pred(32, 3, 8400, n_cand / 8400)
-    for _ in range(3):
-        non_max_suppression(p, 0.25, 0.7)
+def run(counts, nc=3, A=8400, reps=20):
+    B = len(counts)
+    p = pred(B, nc, A, counts).float().contiguous()
+    dev = p.device
+    cap = A
+    cb = torch.empty((B, cap, 4), device=dev); cs = torch.empty((B, cap), device=dev)
+    cc = torch.empty((B, cap), dtype=torch.int32, device=dev); ci = torch.empty((B, cap), dtype=torch.int32, device=dev)
+    cn = torch.zeros((B,), dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    pd = PredCandDesc(p.data_ptr(), B, nc, A, 0.25, 0, None, 0, cb.data_ptr(), cs.data_ptr(), cc.data_ptr(),
+                      ci.data_ptr(), cn.data_ptr(), cap)
+    _lib.check(_lib.lib.ydbl_pred_candidates(pd, s))
+    out = torch.zeros((B, 300, 6), device=dev); cnt = torch.zeros((B,), dtype=torch.int32, device=dev)
+    ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device=dev)
+    nd = NmsDesc(cb.data_ptr(), cs.data_ptr(), cc.data_ptr(), ci.data_ptr(), cn.data_ptr(), B, cap, 0.7, 300, 30000, 0,
+                 7680.0, 640.0, 640.0, out.data_ptr(), cnt.data_ptr(), ws.data_ptr())
+    _lib.check(_lib.lib.ydbl_nms(nd, s))
     torch.cuda.synchronize()
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
-    ev[0].record()
-    for _ in range(10):
-        r = non_max_suppression(p, 0.25, 0.7)
-    ev[1].record()
+    torch.cuda._sleep(int(2e7))
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        _lib.lib.ydbl_nms(nd, s)
+    b.record()
     torch.cuda.synchronize()
-    print(f"cands/img {n_cand:5d}: {ev[0].elapsed_time(ev[1]) / 10 * 1e3:8.1f} us per call (cand+nms+readback), kept {len(r[0])}")
+    return a.elapsed_time(b) / reps * 1e3, cnt.tolist()
+
+
+for label, counts in [("32 x 0", [0] * 32), ("32 x 50", [50] * 32), ("32 x 120", [120] * 32),
+                      ("31 x 120 + 1 x 650", [120] * 31 + [650]), ("32 x 650", [650] * 32),
+                      ("32 x 2000", [2000] * 32), ("32 x 8000", [8000] * 32)]:
+    us, kept = run(counts)
+    print(f"{label:20s}: {us:8.1f} us per ydbl_nms launch   kept {kept[0]}..{kept[-1]}", flush=True)

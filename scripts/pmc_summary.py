@@ -1,57 +1,103 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes per kernel family into profiles/.
+"""Summarise rocprofv3 PMC passes over one bench command per kernel family into profiles/.
 
-    python scripts/pmc_summary.py gpurun_out/pmc1 profiles/r01_pmc_conv_summary.json
+    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<round>_pmc_families.json
 
-HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 for the families whose loads are
-16 B/lane (conv2d, dsconv, dwconv): both counters are in KB and on gfx950 FETCH_SIZE tallies the
-128-B requests of a 16-B/lane streaming read at 64 B (MI355X_MICROARCH.md, HBM section).  The stem
-reads the NCHW image with 4-B/lane loads, for which FETCH_SIZE matched the byte count
-(154.5 MB fetched for a 157 MB input), so it is not doubled.  Infinity-Cache hits are counted.
+Passes (scripts/pmc_families.sh, one counter group per run, --kernel-trace only):
+  FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY
+  SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAVES + GRBM_GUI_ACTIVE.
+HBM bytes per launch = (m * FETCH_SIZE + WRITE_SIZE) KB * 1024, m = 2 for the 16-B/lane loads (gfx950
+FETCH_SIZE tallies a 128-B request of a wide streaming read at 64 B, MI355X_MICROARCH.md HBM section),
+m = 1 for NMS / decode (4-B/lane loads).  Infinity-Cache hits are counted.
+mfma_busy = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): MFMA-busy SIMD cycles over
+the SIMD cycles of the dispatch (GRBM_GUI_ACTIVE is summed over the 8 XCDs).  The summary carries the
+source hash of the HIP code it was measured on; bench.py uses it only when the hash matches.
 """
 import csv
+import glob
+import hashlib
 import json
 import sys
 from collections import defaultdict
+from pathlib import Path
 
-FAMILIES = {  # name keys, FETCH_SIZE multiplier
-    "conv2d": (("conv_igemm_kernel", "conv3x3_tile_kernel", "conv_wsk_kernel", "conv3x3_halo_kernel"), 2),
+ROOT = Path(__file__).resolve().parent.parent
+
+FAMILIES = {  # family -> (kernel-name keys, FETCH_SIZE multiplier)
+    "conv2d": (("conv_igemm_kernel", "conv3x3_tile_kernel", "conv_wsk_kernel", "conv3x3_halo_kernel",
+                "conv3x3_vw_kernel"), 2),
     "dsconv": (("dsconv_kernel",), 2),
-    "stem": (("stem_kernel",), 2),
-    "dwconv": (("dwconv_lds_kernel", "dwconv_kernel"), 2),
+    "dsbottleneck": (("dsbneck_kernel",), 2),
     "bottleneck": (("bneck_kernel",), 2),
     "stem2": (("stem2_kernel",), 2),
+    "stem": (("stem_kernel",), 2),
+    "depthwise": (("dwconv_lds_kernel", "dwconv_kernel", "dw_pair_kernel"), 2),
+    "hypergraph": (("hg_",), 2),
+    "dysample": (("dysample_kernel",), 2),
+    "decode": (("decode_kernel",), 1),
     "nms": (("nms_kernel",), 1),
 }
 
 
-def load(path, counter):
-    per = defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter:
-            continue
-        per[r["Kernel_Name"]].append(float(r["Counter_Value"]))
-    return per
+def code_hash() -> str:
+    """sha256 of the HIP sources + the C-ABI header (the code the counters describe), 12 hex."""
+    h = hashlib.sha256()
+    files = sorted((ROOT / "yolo-dbl_amd" / "csrc").glob("*.hip")) + sorted((ROOT / "yolo-dbl_amd" / "csrc").glob("*.hpp"))
+    files += sorted((ROOT / "include").glob("*.h"))
+    for f in files:
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    return h.hexdigest()[:12]
+
+
+def family(name):
+    for fam, (keys, _) in FAMILIES.items():
+        if any(k in name for k in keys):
+            return fam
+    return None
+
+
+def load(d):
+    """{counter: {family: [values per dispatch]}} over every counter_collection.csv under d."""
+    out = defaultdict(lambda: defaultdict(list))
+    for path in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
+        per = defaultdict(float)  # (dispatch, counter) -> value summed over instances
+        names = {}
+        for r in csv.DictReader(open(path)):
+            key = (r.get("Dispatch_Id") or r.get("Correlation_Id"), r["Counter_Name"])
+            per[key] += float(r["Counter_Value"])
+            names[key] = r["Kernel_Name"]
+        for key, v in per.items():
+            fam = family(names[key])
+            if fam:
+                out[key[1]][fam].append(v)
+    return out
 
 
 def main():
-    d, out = sys.argv[1], sys.argv[2]
-    fetch = load(f"{d}/FETCH_SIZE/run_counter_collection.csv", "FETCH_SIZE")
-    write = load(f"{d}/WRITE_SIZE/run_counter_collection.csv", "WRITE_SIZE")
-    res = {"method": "HBM bytes = (m*FETCH_SIZE + WRITE_SIZE) KB * 1024 per launch; m = 2 for 16-B/lane "
-                     "loads (gfx950 FETCH correction), 1 otherwise", "families": {}}
-    for fam, (keys, mult) in FAMILIES.items():
-        names = [n for n in fetch if any(k in n for k in keys)]
-        nf = sum(len(fetch[n]) for n in names)
-        nw = sum(len(write.get(n, [])) for n in names)
-        if not nf or not nw:
+    d, dst = sys.argv[1], sys.argv[2]
+    c = load(d)
+    res = {"code_hash": code_hash(), "source": d,
+           "method": __doc__.split("\n\n", 1)[1].strip(), "families": {}}
+    for fam, (_, mult) in FAMILIES.items():
+        f, w = c["FETCH_SIZE"].get(fam), c["WRITE_SIZE"].get(fam)
+        if not f or not w:
             continue
-        f_kb = sum(sum(fetch[n]) for n in names) / nf
-        w_kb = sum(sum(write.get(n, [])) for n in names) / nw
-        res["families"][fam] = {"launches": nf, "fetch_kb_per_launch": round(f_kb, 1),
-                                "write_kb_per_launch": round(w_kb, 1),
-                                "fetch_multiplier": mult, "hbm_bytes_per_launch": int((mult * f_kb + w_kb) * 1024)}
-    res["hbm_bytes_per_launch"] = res["families"].get("conv2d", {}).get("hbm_bytes_per_launch")
-    json.dump(res, open(out, "w"), indent=1)
+        e = {"launches": len(f), "fetch_kb_per_launch": round(sum(f) / len(f), 1),
+             "write_kb_per_launch": round(sum(w) / len(w), 1), "fetch_multiplier": mult}
+        e["hbm_bytes_per_launch"] = int((mult * e["fetch_kb_per_launch"] + e["write_kb_per_launch"]) * 1024)
+        mb, gui = c["SQ_VALU_MFMA_BUSY_CYCLES"].get(fam), c["GRBM_GUI_ACTIVE"].get(fam)
+        if mb and gui:
+            e["mfma_busy"] = round(sum(mb) / (1024 * sum(gui) / 8), 4)
+            e["mfma_busy_cycles_per_launch"] = int(sum(mb) / len(mb))
+            e["gui_active_per_launch"] = int(sum(gui) / len(gui))
+        wc = c["SQ_WAVE_CYCLES"].get(fam)
+        if wc:
+            tot = sum(wc)
+            for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
+                if c[k].get(fam):
+                    e[k.lower().replace("sq_", "") + "_frac"] = round(sum(c[k][fam]) / tot, 3)
+        res["families"][fam] = e
+    Path(dst).write_text(json.dumps(res, indent=1) + "\n")
     print(json.dumps(res, indent=1))
 
 

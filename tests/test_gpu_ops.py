@@ -957,6 +957,14 @@ def _rand_pred(n, nc, A, seed, ties=False):
     dict(nc=2, A=4000, conf=0.05, iou=0.6, multi=True),  # 4096 < n <= 8192: LDS sort, global box reads
     dict(nc=1, A=64, conf=0.0, iou=0.0, multi=False),  # iou 0: every overlap suppresses
     dict(nc=3, A=3000, conf=0.2, iou=0.7, multi=False, max_det=1),
+    # m <= 960 sorted candidates: the bitmask path (triangular IoU words, chunk-by-chunk sweep)
+    dict(nc=3, A=900, conf=0.5, iou=0.7, multi=False),            # ~790 candidates, 13 words per row
+    dict(nc=3, A=700, conf=0.25, iou=0.45, multi=False, ties=True),  # equal scores: index order decides
+    dict(nc=3, A=800, conf=0.3, iou=0.6, multi=False, max_det=100),  # max_det reached inside a chunk
+    dict(nc=2, A=400, conf=0.5, iou=0.7, multi=True),              # multi-label, class offsets
+    dict(nc=1, A=500, conf=0.0, iou=0.0, multi=False),             # iou 0 on the bitmask path
+    dict(nc=1, A=65, conf=0.0, iou=0.7, multi=False),              # 65 = one full chunk + 1 row
+    dict(nc=3, A=1040, conf=0.03, iou=0.7, multi=False),           # 960 < m <= 1024: register sort, chunked sweep
 ])
 def test_nms_bit_exact(case):
     from oracle.ops import non_max_suppression as ref_nms

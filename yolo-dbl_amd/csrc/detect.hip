@@ -200,11 +200,51 @@ __device__ void block_bitonic(KP keys, VP vals, int P) {
   }
 }
 
+// Bitonic sort of P <= NMS_THREADS (power of two) keys held one per thread (thread t: element t),
+// values carried along.  Exchanges with partner t ^ j: inside the wave (j < 64) by cross-lane
+// shuffles, no barrier; across waves through two LDS ping-pong buffers, one barrier per stage (a
+// thread reaches stage s+1's barrier only after its stage-s read, so the buffer it overwrites two
+// stages later is no longer read).  log2(P) (log2(P) + 1) / 2 stages, of which only the j >= 64 ones
+// (10 at P = 1024) touch LDS.
+__device__ void reg_bitonic(uint64_t& key, int& val, int P, uint64_t* xk, int* xv) {
+  const int t = threadIdx.x;
+  int stage = 0;
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t ok;
+      int ov;
+      if (j < 64) {
+        const uint32_t lo = __shfl_xor((uint32_t)key, j), hi = __shfl_xor((uint32_t)(key >> 32), j);
+        ok = ((uint64_t)hi << 32) | lo;
+        ov = __shfl_xor(val, j);
+      } else {
+        uint64_t* bk = xk + (stage & 1) * NMS_THREADS;
+        int* bv = xv + (stage & 1) * NMS_THREADS;
+        bk[t] = key;
+        bv[t] = val;
+        __syncthreads();
+        ok = bk[t ^ j];
+        ov = bv[t ^ j];
+        ++stage;
+      }
+      if (t < P) {
+        const bool up = (t & k) == 0, lower = (t & j) == 0;
+        const bool take = (lower == up) ? ok < key : ok > key;
+        if (take) {
+          key = ok;
+          val = ov;
+        }
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4& b, double thr) {
   const float xx1 = fmaxf(a[0], b[0]), yy1 = fmaxf(a[1], b[1]);
   const float xx2 = fminf(a[2], b[2]), yy2 = fminf(a[3], b[3]);
   const float ww = fmaxf(0.f, xx2 - xx1), hh = fmaxf(0.f, yy2 - yy1);
   const float inter = ww * hh;
+  if (!(inter > 0.f)) return false;  // IoU 0 is never > thr (thr in [0, 1])
   const float area_b = (b[2] - b[0]) * (b[3] - b[1]);
   const float uni = (area_a + area_b) - inter;
   // The decision is torchvision's: the correctly rounded fp32 quotient inter / uni, compared in
@@ -240,7 +280,19 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   int P = 64;
   while (P < n) P <<= 1;
   int* order;  // list position -> candidate slot
-  if (in_lds) {
+  if (in_lds && P <= NMS_THREADS) {  // the common case: one candidate per thread, sorted in registers
+    const int t = threadIdx.x;
+    uint64_t key = t < n ? make_key(sc[t], ix[t]) : ~0ull;
+    int val = t < n ? t : -1;
+    if (n > 1) reg_bitonic(key, val, P, s_keys + 2 * NMS_THREADS, s_vals + 2 * NMS_THREADS);
+    __syncthreads();
+    if (t < P) {
+      s_keys[t] = key;
+      s_vals[t] = val;
+    }
+    __syncthreads();
+    order = s_vals;
+  } else if (in_lds) {
     for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
       s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
       s_vals[i] = i < n ? i : -1;
@@ -343,11 +395,19 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     const int ck = s_nk - nk0;
     if (s_nk >= p.max_det) break;
     // (c) suppress every later box against the chunk's kept boxes (all of which precede it).  The
-    // (box, kept box) pairs are spread over the whole workgroup: with R later boxes, G = 1024 / R
-    // thread groups (<= 16) each test every box against every G-th kept box; any hit sets the flag.
+    // (box, kept box) pairs are spread over the whole workgroup: G thread groups (G in 1..16) each test
+    // every box against every G-th kept box, any hit sets the flag; G minimises the per-thread test
+    // count ceil(R G / 1024) * ceil(ck / G) (R later boxes, ck kept boxes).
     const int R = m_cur - (c0 + 64);
     if (R > 0 && ck > 0) {
-      const int G = max(1, min(16, min(ck, NMS_THREADS / R)));
+      int G = 1, best = 1 << 30;
+      for (int g = 1; g <= 16; g <<= 1) {
+        const int cost = ((R * g + NMS_THREADS - 1) / NMS_THREADS) * ((ck + g - 1) / g);
+        if (g <= ck && cost < best) {
+          best = cost;
+          G = g;
+        }
+      }
       const int TS = NMS_THREADS / G;
       const int grp = threadIdx.x / TS, r = threadIdx.x - grp * TS;
       if (grp < G) {
