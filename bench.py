@@ -329,7 +329,9 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--imgsz", type=int, default=640)
     ap.add_argument("--fp32", action="store_true")
-    ap.add_argument("--fp8", action="store_true", help="e4m3 dense-conv operands (BASELINE config 5)")
+    ap.add_argument("--fp8", nargs="?", type=float, const=1.0, default=0.0, metavar="FRACTION",
+                    help="e4m3 dense-conv operands (BASELINE config 5); FRACTION < 1 switches that share of the "
+                         "candidate MACs, least output-sensitive convs first (ydbl.quant.enable_fp8)")
     ap.add_argument("--streams", type=int, default=1,
                     help="sub-batch graphs replayed concurrently on this many HIP streams (DetectSession)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -363,7 +365,8 @@ def main():
     model = YOLO(cfg, nc=3)
     load_trained(model.model, ROOT / "tests" / "golden" / fx)
     B, S = args.batch, args.imgsz
-    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=args.fp8,
+    fp8 = True if args.fp8 >= 1.0 else (args.fp8 if args.fp8 > 0 else False)
+    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=fp8,
                          streams=args.streams)
     if args.fp8:  # activation scales from a separate synthetic calibration batch
         sess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
@@ -385,7 +388,7 @@ def main():
         rf = roofline(sess, dtype_name)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.model, S, B, gpu_session=(model, args.fp8))
+        cpu = cpu_baseline(args.model, S, B, gpu_session=(model, fp8))
     if rank == 0:
         emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu)
     if world > 1:
@@ -433,7 +436,8 @@ def emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu):
         "config": {"workload": f"YOLO-DBL-{args.model} {S}x{S} bs={B}/GPU {dtype_name} forward+decode+NMS "
                                f"(conf .25, iou .7, max_det 300)" + (", RCCL all-gather of boxes" if world > 1 else ""),
                    "model": Path(cfg).stem, "global_batch": B * world, "imgsz": S, "nc": 3,
-                   "parallelism": f"dp{world}", "streams_per_gpu": args.streams},
+                   "parallelism": f"dp{world}", "streams_per_gpu": args.streams,
+                   **({"fp8_mac_fraction": min(args.fp8, 1.0)} if args.fp8 else {})},
         **extra,
         "roofline": rf,
         "cpu_baseline": cpu,

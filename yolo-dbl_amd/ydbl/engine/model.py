@@ -157,7 +157,7 @@ class Model:
         dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
-               bool(fp8), bool(clip), int(streams))
+               float(fp8), bool(clip), int(streams))
         s = self._sessions.get(key)
         if s is None:
             with torch.cuda.device(dev):

@@ -32,6 +32,9 @@ class DetectSession:
             raise ValueError("fp8 operands run on the fp16 activation path (half=True)")
         self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
         self.fp8, self.fp8_ready = bool(fp8), False
+        # fp8=True: every candidate conv in e4m3; fp8=<float in (0, 1)>: that share of the candidates'
+        # MACs, least output-sensitive first (ydbl.quant.enable_fp8)
+        self.fp8_fraction = float(fp8) if not isinstance(fp8, bool) and 0 < float(fp8) < 1 else 1.0
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         self.children = []
         if streams > 1 and batch >= streams:
@@ -129,18 +132,21 @@ class DetectSession:
             raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
         self.compiled.input.copy_(x, non_blocking=True)
 
-    def calibrate_fp8(self, x: torch.Tensor | None = None) -> int:
+    def calibrate_fp8(self, x: torch.Tensor | None = None, fraction: float | None = None) -> int:
         """Switch the dense convs to e4m3 operands (ydbl.quant), with activation scales from one fp16
-        pass over `x` (default: the batch already loaded).  Returns the number of convs switched."""
+        pass over `x` (default: the batch already loaded).  fraction < 1: only that share of the
+        candidates' MACs, least output-sensitive convs first (default: the session's fp8_fraction).
+        Returns the number of convs switched."""
         from ..quant import enable_fp8
 
         if x is not None:
             self.load(x)
+        frac = self.fp8_fraction if fraction is None else float(fraction)
         if self.children:
-            n = sum(c.calibrate_fp8() for c in self.children)
+            n = sum(c.calibrate_fp8(fraction=frac) for c in self.children)
             self.fp8_ready = True
             return n
-        n = enable_fp8(self.plan, self.plan.run)
+        n = enable_fp8(self.plan, self.plan.run, fraction=frac, head=self.compiled.feats)
         self._graph = None  # descriptors changed: recapture
         self.fp8_ready = True
         return n
