@@ -225,10 +225,11 @@ class Model:
     __call__ = predict
 
     def val(self, data=None, **kwargs):
-        """Detection mAP on an in-memory dataset; see ydbl.engine.validator."""
+        """Detection mAP (U/engine/model.py:609-643): ``data`` = a data YAML, a dataset folder, an image folder /
+        list, or in-memory batches; see ydbl.engine.validator.  rect batches by default, like the reference."""
         from .validator import DetectionValidator
 
-        args = {**DEFAULTS, "conf": 0.001, "iou": 0.7, "batch": 16, **kwargs}
+        args = {**DEFAULTS, "conf": 0.001, "iou": 0.7, "batch": 16, "rect": True, "split": "val", **kwargs}
         return DetectionValidator(self, args)(data)
 
 

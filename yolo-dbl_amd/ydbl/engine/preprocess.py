@@ -64,19 +64,33 @@ def letterbox_batch(frames, imgsz=(640, 640), stride=32, pt=True, device="cuda",
     if len(hw) != 1:
         raise ValueError(f"letterboxed frames differ in size {sorted(hw)}; cannot stack")  # np.stack would fail too
     out_h, out_w = hw.pop()
+    meta = np.array([[f.shape[0], f.shape[1], g[0], g[1], g[2], g[4]] for f, g in zip(frames, geo)], dtype=np.int32)
+    return letterbox_frames(frames, meta, out_h, out_w, device=device, pad=pad, out=out)
+
+
+def letterbox_frames(frames, meta, out_h, out_w, device="cuda", pad=114.0, out=None):
+    """ydbl_letterbox with explicit geometry: meta int32 [b, 6] rows (frame h, frame w, resized h, resized w,
+    top, left); each frame is resized (cv2 INTER_LINEAR) to its resized size and placed at (top, left) of an
+    out_h x out_w canvas of `pad`.  Returns fp32 [b, 3, out_h, out_w] RGB /255 on `device`."""
+    meta = np.ascontiguousarray(meta, dtype=np.int32).reshape(-1, 6)
+    b = len(frames)
+    if b == 0 or len(meta) != b:
+        raise ValueError("letterbox_frames: need one meta row per frame")
+    for f, m in zip(frames, meta):
+        if tuple(f.shape[:2]) != (m[0], m[1]) or f.dtype != np.uint8 or f.ndim != 3 or f.shape[2] != 3:
+            raise ValueError("frame does not match its meta row (HWC uint8 BGR)")
+        if m[2] < 1 or m[3] < 1 or m[4] < 0 or m[5] < 0 or m[4] + m[2] > out_h or m[5] + m[3] > out_w:
+            raise ValueError(f"resized frame {tuple(m[2:4])} at {tuple(m[4:6])} does not fit {out_h}x{out_w}")
     sizes = [f.size for f in frames]
     offs = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
     host = torch.empty(int(sum(sizes)), dtype=torch.uint8, pin_memory=True)
     hv = host.numpy()
     for f, o, n in zip(frames, offs, sizes):
         hv[o: o + n] = np.ascontiguousarray(f).reshape(-1)
-    meta = torch.tensor([[f.shape[0], f.shape[1], g[0], g[1], g[2], g[4]] for f, g in zip(frames, geo)],
-                        dtype=torch.int32)
     dev = torch.device(device)
     src = host.to(dev, non_blocking=True)
     offs_d = torch.from_numpy(offs).to(dev)
-    meta_d = meta.to(dev)
-    b = len(frames)
+    meta_d = torch.from_numpy(meta).to(dev)
     if out is None:
         out = torch.empty((b, 3, out_h, out_w), dtype=torch.float32, device=dev)
     elif out.shape != (b, 3, out_h, out_w) or out.dtype != torch.float32 or not out.is_contiguous():
