@@ -42,6 +42,44 @@ def nms_torchvision(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: fl
     n = boxes.shape[0]
     if n == 0:
         return torch.zeros(0, dtype=torch.int64)
+    lib = _c_nms()
+    if lib is not None and not _FORCE_PY_NMS:
+        b = np.ascontiguousarray(boxes.detach().to(torch.float32).cpu().numpy())
+        s = np.ascontiguousarray(scores.detach().to(torch.float32).cpu().numpy())
+        keep = np.empty(n, dtype=np.int64)
+        k = lib.ydbl_oracle_nms(b.ctypes.data, s.ctypes.data, n, float(iou_threshold), keep.ctypes.data)
+        if k < 0:
+            raise MemoryError("ydbl_oracle_nms")
+        return torch.from_numpy(keep[:k].copy())
+    return nms_torchvision_py(boxes, scores, iou_threshold)
+
+
+_FORCE_PY_NMS = False
+_C_NMS = []
+
+
+def _c_nms():
+    """oracle/_nms.so (oracle/nms.c, the same kernel in C, built by `make -C oracle`) when present."""
+    if not _C_NMS:
+        import ctypes
+        from pathlib import Path
+
+        so = Path(__file__).resolve().parent / "_nms.so"
+        lib = None
+        if so.exists():
+            lib = ctypes.CDLL(str(so))
+            lib.ydbl_oracle_nms.restype = ctypes.c_int64
+            lib.ydbl_oracle_nms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_double,
+                                            ctypes.c_void_p]
+        _C_NMS.append(lib)
+    return _C_NMS[0]
+
+
+def nms_torchvision_py(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float) -> torch.Tensor:
+    """nms_torchvision in numpy (the restatement oracle/nms.c is checked against, tests/test_oracle.py)."""
+    n = boxes.shape[0]
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64)
     b = boxes.detach().to(torch.float32).cpu().numpy()
     s = scores.detach().to(torch.float32).cpu().numpy()
     order = np.argsort(-s, kind="stable")  # stable descending (ties keep input order)
