@@ -91,6 +91,9 @@ def main():
             e["mfma_busy_cycles_per_launch"] = int(sum(mb) / len(mb))
             e["gui_active_per_launch"] = int(sum(gui) / len(gui))
         wc = c["SQ_WAVE_CYCLES"].get(fam)
+        if wc and gui:
+            # SQ_WAVE_CYCLES counts quad-cycles summed over resident waves; GRBM_GUI_ACTIVE sums 8 XCDs
+            e["avg_waves_per_cu"] = round(4 * sum(wc) / (sum(gui) / 8) / 256, 2)
         if wc:
             tot = sum(wc)
             for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
