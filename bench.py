@@ -106,7 +106,7 @@ TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("d
            "ydbl_dysample_ex": ("dysample", dysample_traffic)}
 
 
-def roofline(session, dtype_name, reps=3):
+def roofline(session, dtype_name, reps=3, key=None):
     """Per-launch HIP-event timing of one eager walk of every plan of the session (min of `reps`); the
     dominant kernel family (most time) = the dense conv; a per-family table beside it."""
     elsize = 4 if dtype_name == "fp32" else 2  # activation bytes (fp8 mode keeps fp16 activations)
@@ -131,7 +131,7 @@ def roofline(session, dtype_name, reps=3):
             e["bytes"] += b
             e["flops"] += f
     pk = MFMA_PEAK_TFLOPS[dtype_name]
-    pmc = pmc_summary()
+    pmc = pmc_summary(key)
     families = {}
     for name, e in sorted(fam.items(), key=lambda kv: -kv[1]["ms"]):
         gbs = e["bytes"] / (e["ms"] * 1e-3) / 1e9
@@ -163,7 +163,7 @@ def roofline(session, dtype_name, reps=3):
                "ms_by_kernel": {k: round(v, 3) for k, v in sorted(by_kind.items(), key=lambda kv: -kv[1])},
                "traffic": pc.get("hbm_bytes_per_launch"), "mfma_busy": pc.get("mfma_busy"),
                "code_hash": code_hash(),
-               "pmc_summary": pmc["file"] if pmc else "none for this code hash (scripts/pmc_families.sh)",
+               "pmc_summary": pmc["file"] if pmc else "none for this code hash and workload (scripts/pmc_families.sh)",
                "families": families})
     return rf
 
@@ -175,15 +175,21 @@ def code_hash() -> str:
     return ch()
 
 
-def pmc_summary():
-    """The newest committed profiles/*_pmc_families.json measured on THIS code (matching source hash)."""
+def workload_key(args, dtype_name) -> str:
+    """What a PMC summary must have been measured on to describe this run's launches."""
+    return f"model={args.model} batch={args.batch} imgsz={args.imgsz} dtype={dtype_name} streams={args.streams}"
+
+
+def pmc_summary(key=None):
+    """The newest committed profiles/*_pmc_families.json measured on THIS code (matching source hash) and,
+    when `key` is given, on this workload (scripts/pmc_families.sh records bench.py's workload_key)."""
     h = code_hash()
     for p in sorted((ROOT / "profiles").rglob("*_pmc_families.json"), reverse=True):
         try:
             d = json.loads(p.read_text())
         except Exception:
             continue
-        if d.get("code_hash") == h:
+        if d.get("code_hash") == h and (key is None or d.get("workload") == key):
             d["file"] = str(p.relative_to(ROOT))
             return d
     return None
@@ -332,8 +338,9 @@ def main():
     ap.add_argument("--fp8", nargs="?", type=float, const=1.0, default=0.0, metavar="FRACTION",
                     help="e4m3 dense-conv operands (BASELINE config 5); FRACTION < 1 switches that share of the "
                          "candidate MACs, least output-sensitive convs first (ydbl.quant.enable_fp8)")
-    ap.add_argument("--streams", type=int, default=1,
-                    help="sub-batch graphs replayed concurrently on this many HIP streams (DetectSession)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="sub-batch graphs replayed concurrently on this many HIP streams (DetectSession); "
+                         "2 measured +3 %% DBL-n bs32, +9 %% DBL-s bs64, +8.5 %% DBL-l 1280 bs8 over 1 (4: -33 %% DBL-n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stub-cpu", action="store_true", help="gloo/CPU plumbing check of the N-rank launch (no GPU)")
@@ -380,12 +387,15 @@ def main():
             gather_detections(det, cnt, B * world)
 
     el = timed_steps(step, args, world, lambda: torch.cuda.synchronize(dev), dev)
+    key = workload_key(args, dtype_name)
+    if rank == 0 and os.environ.get("YDBL_WORKLOAD_KEY_OUT"):  # scripts/pmc_families.sh
+        Path(os.environ["YDBL_WORKLOAD_KEY_OUT"]).write_text(key)
     extra = {"dets_per_image": round(float(sess.count.float().mean().item()), 2),
              "candidates_per_image": round(float(sess.cand_count.float().mean().item()), 1),
              "candidates_max": int(sess.cand_count.max().item())}
     rf = None
     if rank == 0 and not args.no_roofline:
-        rf = roofline(sess, dtype_name)
+        rf = roofline(sess, dtype_name, key=key)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, S, B, gpu_session=(model, fp8))

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 PMC passes over one bench command per kernel family into profiles/.
 
-    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<round>_pmc_families.json
+    python scripts/pmc_summary.py gpurun_out/<tag> profiles/<round>_pmc_families.json ["<bench workload_key>"]
 
 Passes (scripts/pmc_families.sh, one counter group per run, --kernel-trace only):
   FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY
@@ -76,7 +76,7 @@ def load(d):
 def main():
     d, dst = sys.argv[1], sys.argv[2]
     c = load(d)
-    res = {"code_hash": code_hash(), "source": d,
+    res = {"code_hash": code_hash(), "workload": sys.argv[3] if len(sys.argv) > 3 else None, "source": d,
            "method": __doc__.split("\n\n", 1)[1].strip(), "families": {}}
     for fam, (_, mult) in FAMILIES.items():
         f, w = c["FETCH_SIZE"].get(fam), c["WRITE_SIZE"].get(fam)
