@@ -31,7 +31,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = {"fp16": 2500.0, "fp32": 157.3, "fp8": 5000.0}
 CFGS = {"n": ("yolov13n_DBL.yaml", "trained_yolov13n_DBL_nc3.npz"),
         "s": ("yolov13s_DBL.yaml", "trained_yolov13s_DBL_nc3.npz"),
-        "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc3.npz")}
+        "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc3.npz"),
+        "x": ("yolov13x_DBL2.yaml", "trained_yolov13x_DBL2_nc3.npz")}
 
 
 def _px(v):

@@ -1,6 +1,6 @@
 """Generate the end-to-end parity fixtures tests/golden/e2e_<model><size>.npz (run in the CPU container).
 
-For each BASELINE model/size (DBL-n 640, DBL-s 640, DBL-l(DBL2) 1280) the oracle restatement
+For each BASELINE model/size (DBL-n 640, DBL-s 640, DBL-l(DBL2) 1280, and DBL-x(DBL2) 640) the oracle restatement
 (oracle/model.py; nothing from the reference is run) evaluates the first reference images of the
 synthetic batch blob_images(B_full, S, seed=1234) on the trained-like state_dict fixture in three
 precisions.  Stored:
@@ -30,7 +30,8 @@ from parity_util import (detections, err_stats, fp16_rule, fp32_rule, match_dete
 from ydbl.utils.synthetic import blob_images  # noqa: E402
 
 OUT = Path(__file__).resolve().parent
-CASES = {"n640": ("n", 640, 32, [0, 1]), "s640": ("s", 640, 32, [0, 1]), "l1280": ("l", 1280, 8, [0])}
+CASES = {"n640": ("n", 640, 32, [0, 1]), "s640": ("s", 640, 32, [0, 1]), "l1280": ("l", 1280, 8, [0]),
+         "x640": ("x", 640, 8, [0])}
 
 
 def choose_conf(y64):

@@ -16,7 +16,7 @@ every expected output comes from the oracle restatement in ``oracle/``.
    conf .05 so that the small images keep some boxes, iou .7) and val
    (conf .001, multi-label) settings.
 
-Usage: python tests/golden/make_golden.py
+Usage: python tests/golden/make_golden.py [cfg nc]   (cfg nc: regenerate that one trained-like fixture only)
 """
 
 from __future__ import annotations
@@ -38,7 +38,7 @@ from ydbl.utils.synthetic import blob_images  # noqa: E402  (pure tensor utility
 
 OUT = Path(__file__).resolve().parent
 CONFIGS = [("yolov13n_DBL.yaml", 3), ("yolov13n_DBL.yaml", 80), ("yolov13s_DBL.yaml", 3), ("yolov13s_DBL.yaml", 80),
-           ("yolov13l_DBL2.yaml", 3)]
+           ("yolov13l_DBL2.yaml", 3), ("yolov13x_DBL2.yaml", 3)]
 
 
 def trained_keys(model):
@@ -91,8 +91,10 @@ def make_trained(cfg: str, nc: int, calib_size=320, calib_n=8):
     return m, arrays
 
 
-def main():
+def main(only=None):
     for cfg, nc in CONFIGS:
+        if only and (cfg, nc) != only:
+            continue
         m, arrays = make_trained(cfg, nc)
         stem = Path(cfg).stem
         np.savez_compressed(OUT / f"trained_{stem}_nc{nc}.npz", **arrays)
@@ -101,6 +103,8 @@ def main():
             y, _ = m.fuse()(x)
             frac = (y[:, 4:].amax(1) > 0.25).float().mean().item()
         print(f"{cfg} nc={nc}: {len(arrays)} arrays; anchors with max score > .25 at 640: {frac:.3%}")
+    if only:
+        return
 
     # golden vectors (DBL-n, nc=3, 128x128, bs 2)
     m, _ = make_trained("yolov13n_DBL.yaml", 3)
@@ -119,4 +123,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main((sys.argv[1], int(sys.argv[2])) if len(sys.argv) > 2 else None)

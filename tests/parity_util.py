@@ -23,7 +23,8 @@ from oracle.ops import clip_boxes, non_max_suppression
 
 ROLE_FX = {"n": ("yolov13n_DBL.yaml", "trained_yolov13n_DBL_nc{nc}.npz"),
            "s": ("yolov13s_DBL.yaml", "trained_yolov13s_DBL_nc{nc}.npz"),
-           "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc{nc}.npz")}
+           "l": ("yolov13l_DBL2.yaml", "trained_yolov13l_DBL2_nc{nc}.npz"),
+           "x": ("yolov13x_DBL2.yaml", "trained_yolov13x_DBL2_nc{nc}.npz")}
 
 
 def build_pair(scale: str, nc: int, golden_dir):

@@ -64,7 +64,7 @@ def _run(golden_dir, name, batch, mode, streams=1):
 
 
 @pytest.mark.parametrize("name,batch", [("n640", 32), ("n640", 2), ("s640", 2), ("s640", 32), ("l1280", 1),
-                                        ("l1280", 8)])
+                                        ("l1280", 8), ("x640", 8)])
 def test_e2e_fp32(golden_dir, name, batch):
     y64, meta, yg, dets, ref_dets = _run(golden_dir, name, batch, "fp32")
     o32 = meta["oracle_fp32"]
@@ -82,7 +82,7 @@ def test_e2e_fp32(golden_dir, name, batch):
 
 
 @pytest.mark.parametrize("name,batch,streams", [("n640", 32, 1), ("n640", 32, 2), ("n640", 2, 1), ("s640", 8, 1),
-                                                ("s640", 32, 2), ("l1280", 8, 1)])
+                                                ("s640", 32, 2), ("l1280", 8, 1), ("x640", 8, 2)])
 def test_e2e_fp16(golden_dir, name, batch, streams):
     """streams=2: the bench's layout (two bs/2 sub-batch graphs replayed on two HIP streams)."""
     y64, meta, yg, dets, ref_dets = _run(golden_dir, name, batch, "fp16", streams)

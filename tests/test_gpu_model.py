@@ -33,7 +33,7 @@ def _models(cfg, nc, golden_dir):
 
 @pytest.mark.parametrize("cfg,nc,size", [("yolov13n_DBL.yaml", 3, 128), ("yolov13n_DBL.yaml", 80, 160),
                                          ("yolov13s_DBL.yaml", 3, 128), ("yolov13s_DBL.yaml", 80, 160),
-                                         ("yolov13l_DBL2.yaml", 3, 128)])
+                                         ("yolov13l_DBL2.yaml", 3, 128), ("yolov13x_DBL2.yaml", 3, 128)])
 def test_model_fp32_parity(cfg, nc, size, golden_dir):
     """Small-size companion of tests/test_gpu_e2e.py (which runs the BASELINE shapes): raw per-level head
     outputs, decoded predictions and final detections vs the oracle's fp64 answer, bounded by twice the
