@@ -31,7 +31,7 @@ from ydbl.utils.synthetic import blob_images  # noqa: E402
 
 OUT = Path(__file__).resolve().parent
 CASES = {"n640": ("n", 640, 32, [0, 1]), "s640": ("s", 640, 32, [0, 1]), "l1280": ("l", 1280, 8, [0]),
-         "x640": ("x", 640, 8, [0])}
+         "x640": ("x", 640, 8, [0, 1])}
 
 
 def choose_conf(y64):
