@@ -11,19 +11,24 @@ from ydbl import _lib  # noqa: E402
 from ydbl._lib import NmsDesc, PredCandDesc  # noqa: E402
 
 
-def pred(B, nc, A, counts, seed=0):
+def pred(B, nc, A, counts, seed=0, spread=False):
     g = torch.Generator().manual_seed(seed)
     xy = torch.rand(B, 2, A, generator=g) * 600 + 20
     wh = torch.rand(B, 2, A, generator=g) * 80 + 4
     sc = torch.rand(B, nc, A, generator=g) * 0.2
     for b, k in enumerate(counts):
-        sc[b, 0, :k] = 0.3 + 0.7 * torch.rand(k, generator=g)
+        if spread:  # candidate i belongs to class i % nc
+            for c in range(nc):
+                idx = torch.arange(c, k, nc)
+                sc[b, c, idx] = 0.3 + 0.7 * torch.rand(len(idx), generator=g)
+        else:
+            sc[b, 0, :k] = 0.3 + 0.7 * torch.rand(k, generator=g)
     return torch.cat([xy, wh, sc], 1).cuda()
 
 
-def run(counts, nc=3, A=8400, reps=20):
+def run(counts, nc=3, A=8400, reps=20, spread=False):
     B = len(counts)
-    p = pred(B, nc, A, counts).float().contiguous()
+    p = pred(B, nc, A, counts, spread=spread).float().contiguous()
     dev = p.device
     cap = A
     cb = torch.empty((B, cap, 4), device=dev); cs = torch.empty((B, cap), device=dev)
@@ -49,8 +54,10 @@ def run(counts, nc=3, A=8400, reps=20):
     return a.elapsed_time(b) / reps * 1e3, cnt.tolist()
 
 
-for label, counts in [("32 x 0", [0] * 32), ("32 x 50", [50] * 32), ("32 x 120", [120] * 32),
-                      ("31 x 120 + 1 x 650", [120] * 31 + [650]), ("32 x 650", [650] * 32),
-                      ("32 x 2000", [2000] * 32), ("32 x 8000", [8000] * 32)]:
-    us, kept = run(counts)
-    print(f"{label:20s}: {us:8.1f} us per ydbl_nms launch   kept {kept[0]}..{kept[-1]}", flush=True)
+cases = [("32 x 0", [0] * 32, 3, False), ("32 x 120", [120] * 32, 3, False),
+         ("31 x 120 + 1 x 650", [120] * 31 + [650], 3, False), ("32 x 650", [650] * 32, 3, False),
+         ("32 x 2000", [2000] * 32, 3, False), ("31x120+1x650 nc3 spread", [120] * 31 + [650], 3, True),
+         ("32 x 650 nc3 spread", [650] * 32, 3, True), ("32 x 2000 nc80 spread", [2000] * 32, 80, True)]
+for label, counts, nc, spread in cases:
+    us, kept = run(counts, nc=nc, spread=spread)
+    print(f"{label:26s}: {us:8.1f} us per ydbl_nms launch   kept {kept[0]}..{kept[-1]}", flush=True)

@@ -965,11 +965,18 @@ def _rand_pred(n, nc, A, seed, ties=False):
     dict(nc=1, A=500, conf=0.0, iou=0.0, multi=False),             # iou 0 on the bitmask path
     dict(nc=1, A=65, conf=0.0, iou=0.7, multi=False),              # 65 = one full chunk + 1 row
     dict(nc=3, A=1040, conf=0.03, iou=0.7, multi=False),           # 960 < m <= 1024: register sort, chunked sweep
+    dict(nc=80, A=8400, conf=0.05, iou=0.7, multi=False, max_det=300),  # many classes: groups of 10 classes
+    dict(nc=17, A=3000, conf=0.02, iou=0.6, multi=True, max_det=40),    # max_det cut across the merged lists
+    dict(nc=9, A=2500, conf=0.01, iou=0.7, multi=True, max_nms=1500),   # max_nms: whole image in group 0
 ])
-def test_nms_bit_exact(case):
+@pytest.mark.parametrize("groups", ["1", "0"])
+def test_nms_bit_exact(case, groups, monkeypatch):
+    """groups "1": the class-split sweep (8 class-group workgroups per image + merge), "0": one workgroup
+    per image; both bit-exact against the restated torchvision semantics."""
     from oracle.ops import non_max_suppression as ref_nms
     from ydbl.utils.ops import non_max_suppression
 
+    monkeypatch.setenv("YDBL_NMS_GROUPS", groups)
     case = dict(case)
     nc, A = case.pop("nc"), case.pop("A")
     pred = _rand_pred(3, nc, A, seed=A + nc, ties=case.pop("ties", False))

@@ -9,6 +9,8 @@
 //          1024-thread workgroup per image runs the greedy sweep with the suppression flags and
 //          the first 4096 sorted boxes in LDS.  The sweep stops after max_det keeps, which is the
 //          same as the reference's keep[:max_det] because keeps are produced in score order.
+#include <stdlib.h>
+
 #include "common.hpp"
 
 #pragma clang fp contract(off)
@@ -171,9 +173,12 @@ __device__ __forceinline__ uint64_t make_key(float score, int idx) {
   return ((uint64_t)(0xFFFFFFFFu - sb) << 32) | (uint32_t)idx;
 }
 
+constexpr int NMS_GROUPS = 8;  // class groups (cls % 8) swept by separate workgroups
+
 struct NmsArgs {
   const float* cbox; const float* cscore; const int* ccls; const int* cidx; const int* ccount;
   uint64_t* gkeys; int* gvals; int L;  // global sort scratch (only when cap > NMS_SORT_LDS)
+  int* gslot; uint64_t* gkey; int* gcount; int gk;  // per (image, class group) keep lists, gk entries each
   int cap;
   double thr; int max_det, max_nms; float off_scale;
   float clip_w, clip_h;
@@ -258,6 +263,26 @@ __device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4
   return (double)ovr > thr;
 }
 
+// Diagnostic build only (-DYDBL_NMS_STAMPS, scripts/nms_stamps.sh): per-workgroup phase timestamps.
+#ifdef YDBL_NMS_STAMPS
+__device__ unsigned long long g_nms_stamps[16 * 4096];
+#define NMS_STAMP(k, v) \
+  do { if (threadIdx.x == 0) g_nms_stamps[blockIdx.x * 16 + (k)] = (v); } while (0)
+#define NMS_TICK(acc) \
+  do { const unsigned long long t_ = __builtin_amdgcn_s_memrealtime(); acc += t_ - t_last; t_last = t_; } while (0)
+#else
+#define NMS_STAMP(k, v) do { } while (0)
+#define NMS_TICK(acc) do { } while (0)
+#endif
+
+// GROUPS: the class-split form (non-agnostic NMS).  Boxes are offset by cls * max_wh, so boxes of
+// different classes never overlap and torchvision's greedy sweep is, class by class, independent: the
+// keep set of an image is the union of the keep sets of any partition of its classes, in (score, index)
+// order.  Workgroup (image b, group g) runs the sweep on the candidates with cls % NMS_GROUPS == g and
+// leaves its keep list (slots + sort keys, at most max_det) in the workspace; nms_merge_kernel ranks the
+// groups' lists into the final max_det rows.  An image whose candidates exceed max_nms (the reference's
+// global pre-NMS truncation) or the LDS sort runs whole in group 0 (the other groups leave empty lists).
+template <bool GROUPS>
 __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   // LDS: sort keys (64 KB) are reused for the first 4096 sorted boxes after sorting.
   __shared__ __align__(16) uint64_t s_keys[NMS_SORT_LDS];
@@ -266,15 +291,47 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   __shared__ int kept_slot[NMS_MAX_DET];
   __shared__ int s_wsum[NMS_THREADS / 64];
   __shared__ f32x4 chunk_box[64];
+  __shared__ float chunk_area[64];
   __shared__ unsigned char cmask[64][16];
   __shared__ int s_nk;
   f32x4* s_box = reinterpret_cast<f32x4*>(s_keys);
   constexpr int LDS_BOXES = NMS_SORT_LDS * 8 / 16;
 
-  const int b = blockIdx.x;
-  const int n = min(p.ccount[b], p.cap);
+  NMS_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  const int b = GROUPS ? blockIdx.x / NMS_GROUPS : blockIdx.x;
+  const int grp = GROUPS ? blockIdx.x % NMS_GROUPS : 0;
+  int n = min(p.ccount[b], p.cap);
   const float* sc = p.cscore + (int64_t)b * p.cap;
   const int* ix = p.cidx + (int64_t)b * p.cap;
+  bool listed = false;  // GROUPS: this group's (key, slot) list is already in s_keys / s_vals
+  if constexpr (GROUPS) {
+    const int64_t gi = (int64_t)b * NMS_GROUPS + grp;
+    if (n > p.max_nms || n > NMS_SORT_LDS) {  // whole image in group 0
+      if (grp != 0) {
+        if (threadIdx.x == 0) p.gcount[gi] = 0;
+        return;
+      }
+    } else {
+      const int* cc = p.ccls + (int64_t)b * p.cap;
+      if (threadIdx.x == 0) s_nk = 0;
+      __syncthreads();
+      for (int t = threadIdx.x; t < n; t += NMS_THREADS) {
+        if (cc[t] % NMS_GROUPS == grp) {  // list order is free: the sort key orders it
+          const int pos = atomicAdd(&s_nk, 1);
+          s_keys[pos] = make_key(sc[t], ix[t]);
+          s_vals[pos] = t;
+        }
+      }
+      __syncthreads();
+      n = s_nk;
+      __syncthreads();
+      listed = true;
+      if (n == 0) {
+        if (threadIdx.x == 0) p.gcount[gi] = 0;
+        return;
+      }
+    }
+  }
   // ---- 1. sort
   const bool in_lds = n <= NMS_SORT_LDS;
   int P = 64;
@@ -282,8 +339,12 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   int* order;  // list position -> candidate slot
   if (in_lds && P <= NMS_THREADS) {  // the common case: one candidate per thread, sorted in registers
     const int t = threadIdx.x;
-    uint64_t key = t < n ? make_key(sc[t], ix[t]) : ~0ull;
-    int val = t < n ? t : -1;
+    uint64_t key = ~0ull;
+    int val = -1;
+    if (t < n) {
+      key = listed ? s_keys[t] : make_key(sc[t], ix[t]);
+      val = listed ? s_vals[t] : t;
+    }
     if (n > 1) reg_bitonic(key, val, P, s_keys + 2 * NMS_THREADS, s_vals + 2 * NMS_THREADS);
     __syncthreads();
     if (t < P) {
@@ -294,8 +355,10 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     order = s_vals;
   } else if (in_lds) {
     for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
-      s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
-      s_vals[i] = i < n ? i : -1;
+      if (!listed || i >= n) {
+        s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+        s_vals[i] = i < n ? i : -1;
+      }
     }
     __syncthreads();
     if (n > 1) block_bitonic(s_keys, s_vals, P);
@@ -312,6 +375,8 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     order = gv;
   }
   const int m = min(n, p.max_nms);
+  NMS_STAMP(1, __builtin_amdgcn_s_memrealtime());
+  NMS_STAMP(6, (unsigned long long)m);
   // ---- stage boxes (class-offset) of the first LDS_BOXES sorted candidates; flags
   const float* cb = p.cbox + (int64_t)b * p.cap * 4;
   const int* cc = p.ccls + (int64_t)b * p.cap;
@@ -347,7 +412,13 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;  // 16 waves
   int m_cur = m;
+  NMS_STAMP(2, __builtin_amdgcn_s_memrealtime());
+  int rounds = 0;
+#ifdef YDBL_NMS_STAMPS
+  unsigned long long t_last = __builtin_amdgcn_s_memrealtime(), ta = 0, tb = 0, tc = 0, td = 0;
+#endif
   for (int c0 = 0; c0 < m_cur;) {
+    ++rounds;
     const int nk0 = s_nk;
     if (nk0 >= p.max_det) break;
     // (a) intra-chunk suppression masks: wave w tests columns c0+4w..c0+4w+3 against row c0+lane
@@ -368,6 +439,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       cmask[lane][wave] = (unsigned char)bits;
     }
     __syncthreads();
+    NMS_TICK(ta);
     // (b) wave 0 resolves the chunk on scalar registers only (find-first-set, readlane of the kept
     // row's mask, and-not), then every lane places itself by the rank of its bit in the kept mask
     if (wave == 0) {
@@ -388,12 +460,14 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
         const int rank = __popcll(K & ((1ull << lane) - 1));
         kept_slot[nk0 + rank] = order[i];
         chunk_box[rank] = bi;
+        chunk_area[rank] = (bi[2] - bi[0]) * (bi[3] - bi[1]);
       }
       if (lane == 0) s_nk = nk;
     }
     __syncthreads();
     const int ck = s_nk - nk0;
     if (s_nk >= p.max_det) break;
+    NMS_TICK(tb);
     // (c) suppress every later box against the chunk's kept boxes (all of which precede it).  The
     // (box, kept box) pairs are spread over the whole workgroup: G thread groups (G in 1..16) each test
     // every box against every G-th kept box, any hit sets the flag; G minimises the per-thread test
@@ -409,23 +483,33 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
         }
       }
       const int TS = NMS_THREADS / G;
-      const int grp = threadIdx.x / TS, r = threadIdx.x - grp * TS;
-      if (grp < G) {
+      const int tg = threadIdx.x / TS, r = threadIdx.x - tg * TS;
+      if (tg < G) {
         for (int j = c0 + 64 + r; j < m_cur; j += TS) {
           if (removed[j]) continue;
           const f32x4 bj = box_at(j);
-          for (int q = grp; q < ck; q += G) {
-            const f32x4 bq = chunk_box[q];
-            const float aq = (bq[2] - bq[0]) * (bq[3] - bq[1]);
-            if (iou_gt(bq, aq, bj, p.thr)) {
-              removed[j] = 1;
-              break;
+          // kept boxes in batches of 8: the 8 broadcast LDS reads are in flight together and the tests
+          // are independent (any hit suppresses; testing past the first hit changes nothing)
+          bool sup = false;
+          for (int q0 = tg; q0 < ck && !sup; q0 += 8 * G) {
+            f32x4 bq[8];
+            float aq[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+              const int q = min(q0 + u * G, ck - 1);
+              bq[u] = chunk_box[q];
+              aq[u] = chunk_area[q];
             }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+              if (q0 + u * G < ck) sup |= iou_gt(bq[u], aq[u], bj, p.thr);
           }
+          if (sup) removed[j] = 1;
         }
       }
     }
     __syncthreads();
+    NMS_TICK(tc);
     if (!compact) {
       c0 += 64;
       continue;
@@ -476,10 +560,27 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       }
     }
     m_cur = total;
+    NMS_TICK(td);
     __syncthreads();
   }
   __syncthreads();
+  NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
+  NMS_STAMP(5, (unsigned long long)rounds);
+#ifdef YDBL_NMS_STAMPS
+  NMS_STAMP(7, ta); NMS_STAMP(8, tb); NMS_STAMP(9, tc); NMS_STAMP(10, td);
+#endif
   const int kept = min(s_nk, p.max_det);
+  if constexpr (GROUPS) {  // this group's keep list for nms_merge_kernel
+    const int64_t gi = (int64_t)b * NMS_GROUPS + grp;
+    for (int k = threadIdx.x; k < kept; k += NMS_THREADS) {
+      const int slot = kept_slot[k];
+      const int64_t o = (int64_t)b * p.cap + slot;
+      p.gslot[gi * p.gk + k] = slot;
+      p.gkey[gi * p.gk + k] = make_key(p.cscore[o], p.cidx[o]);
+    }
+    if (threadIdx.x == 0) p.gcount[gi] = kept;
+    return;
+  }
   for (int k = threadIdx.x; k < kept; k += NMS_THREADS) {
     const int slot = kept_slot[k];
     const int64_t o = (int64_t)b * p.cap + slot;
@@ -498,6 +599,76 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     dst[5] = float(p.ccls[o]);
   }
   // rows kept..max_det of the fixed-shape output are zeroed (the all-gather ships whole buffers)
+  float* rest = p.out + ((int64_t)b * p.max_det + kept) * 6;
+  for (int k = threadIdx.x; k < (p.max_det - kept) * 6; k += NMS_THREADS) rest[k] = 0.f;
+  if (threadIdx.x == 0) p.out_count[b] = kept;
+}
+
+// The groups' keep lists of one image, each in (score, index) order, merged into the first max_det rows:
+// an entry's final row is its position in its own list plus the number of entries of every other list
+// with a smaller key (keys are unique: they carry the candidate's original index), found by binary
+// search over the lists staged in LDS.  Entries ranked past max_det are dropped, the rest of the
+// fixed-shape output is zeroed.
+constexpr int NMS_MERGE_LDS = 8192;
+__global__ __launch_bounds__(NMS_THREADS) void nms_merge_kernel(NmsArgs p) {
+  __shared__ uint64_t s_key[NMS_MERGE_LDS];
+  __shared__ int s_cnt[NMS_GROUPS], s_off[NMS_GROUPS + 1];
+  const int b = blockIdx.x;
+  const int64_t g0 = (int64_t)b * NMS_GROUPS;
+  if (threadIdx.x == 0) {
+    int o = 0;
+    for (int g = 0; g < NMS_GROUPS; ++g) {
+      s_cnt[g] = p.gcount[g0 + g];
+      s_off[g] = o;
+      o += s_cnt[g];
+    }
+    s_off[NMS_GROUPS] = o;
+  }
+  __syncthreads();
+  const int E = s_off[NMS_GROUPS];
+  const bool in_lds = E <= NMS_MERGE_LDS;
+  if (in_lds) {
+    for (int g = 0; g < NMS_GROUPS; ++g)
+      for (int j = threadIdx.x; j < s_cnt[g]; j += NMS_THREADS) s_key[s_off[g] + j] = p.gkey[(g0 + g) * p.gk + j];
+    __syncthreads();
+  }
+  auto key_at = [&](int g, int j) -> uint64_t {
+    return in_lds ? s_key[s_off[g] + j] : p.gkey[(g0 + g) * p.gk + j];
+  };
+  for (int e = threadIdx.x; e < E; e += NMS_THREADS) {
+    int g = 0;
+    while (e >= s_off[g + 1]) ++g;
+    const int j = e - s_off[g];
+    const uint64_t key = key_at(g, j);
+    int rank = j;
+    for (int h = 0; h < NMS_GROUPS; ++h) {
+      if (h == g) continue;
+      int lo = 0, hi = s_cnt[h];  // number of keys of list h below `key`
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (key_at(h, mid) < key) lo = mid + 1;
+        else hi = mid;
+      }
+      rank += lo;
+    }
+    if (rank >= p.max_det) continue;
+    const int slot = p.gslot[(g0 + g) * p.gk + j];
+    const int64_t o = (int64_t)b * p.cap + slot;
+    f32x4 v = *reinterpret_cast<const f32x4*>(p.cbox + o * 4);
+    if (p.clip_w > 0.f) {
+      v[0] = fminf(fmaxf(v[0], 0.f), p.clip_w);
+      v[2] = fminf(fmaxf(v[2], 0.f), p.clip_w);
+    }
+    if (p.clip_h > 0.f) {
+      v[1] = fminf(fmaxf(v[1], 0.f), p.clip_h);
+      v[3] = fminf(fmaxf(v[3], 0.f), p.clip_h);
+    }
+    float* dst = p.out + ((int64_t)b * p.max_det + rank) * 6;
+    dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
+    dst[4] = p.cscore[o];
+    dst[5] = float(p.ccls[o]);
+  }
+  const int kept = min(E, p.max_det);
   float* rest = p.out + ((int64_t)b * p.max_det + kept) * 6;
   for (int k = threadIdx.x; k < (p.max_det - kept) * 6; k += NMS_THREADS) rest[k] = 0.f;
   if (threadIdx.x == 0) p.out_count[b] = kept;
@@ -578,10 +749,21 @@ extern "C" int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream) 
   return check_launch("ydbl_pred_candidates");
 }
 
+// [global sort keys n*L x 8 B][sort slots n*L x 4 B][group keys n*G*gk x 8 B][group slots x 4 B][counts n*G x 4 B]
+static int64_t nms_sort_len(int32_t cap) { return cap <= NMS_SORT_LDS ? 0 : next_pow2(cap); }
+static int32_t nms_group_len(int32_t cap) { return cap < NMS_MAX_DET ? cap : NMS_MAX_DET; }
+
+#ifdef YDBL_NMS_STAMPS
+extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nms_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms) {
   (void)max_nms;
-  if (cap <= NMS_SORT_LDS) return 16;
-  return (int64_t)n * next_pow2(cap) * (8 + 4);
+  if (n < 1 || cap < 1) return 16;
+  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap);
+  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 16;
 }
 
 extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
@@ -597,14 +779,25 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   NmsArgs a;
   a.cbox = d->cand_box; a.cscore = d->cand_score; a.ccls = d->cand_cls; a.cidx = d->cand_idx;
   a.ccount = d->cand_count;
-  a.L = d->cap <= NMS_SORT_LDS ? 0 : next_pow2(d->cap);
+  a.L = (int)nms_sort_len(d->cap);
   a.gkeys = reinterpret_cast<uint64_t*>(d->workspace);
   a.gvals = reinterpret_cast<int*>(a.gkeys + (int64_t)d->n * a.L);
+  a.gk = nms_group_len(d->cap);
+  a.gkey = reinterpret_cast<uint64_t*>(a.gvals + (int64_t)d->n * a.L + ((int64_t)d->n * a.L & 1));  // 8-B aligned
+  a.gslot = reinterpret_cast<int*>(a.gkey + (int64_t)d->n * NMS_GROUPS * a.gk);
+  a.gcount = a.gslot + (int64_t)d->n * NMS_GROUPS * a.gk;
   a.cap = d->cap;
   a.thr = d->iou_thres; a.max_det = d->max_det; a.max_nms = d->max_nms;
   a.off_scale = d->agnostic ? 0.f : d->max_wh;
   a.clip_w = d->clip_w; a.clip_h = d->clip_h;
   a.out = d->out; a.out_count = d->out_count;
-  nms_kernel<<<d->n, NMS_THREADS, 0, s>>>(a);
+  // class-split sweep + merge (non-agnostic); the one-workgroup-per-image form for agnostic NMS or on request
+  const char* ev = getenv("YDBL_NMS_GROUPS");  // A/B switch (read per launch: tests): 0 = one workgroup per image
+  if (d->agnostic || (ev && *ev == '0')) {
+    nms_kernel<false><<<d->n, NMS_THREADS, 0, s>>>(a);
+  } else {
+    nms_kernel<true><<<(unsigned)((int64_t)d->n * NMS_GROUPS), NMS_THREADS, 0, s>>>(a);
+    nms_merge_kernel<<<d->n, NMS_THREADS, 0, s>>>(a);
+  }
   return check_launch("ydbl_nms");
 }
