@@ -396,7 +396,19 @@ def main():
              "candidates_max": int(sess.cand_count.max().item())}
     rf = None
     if rank == 0 and not args.no_roofline:
-        rf = roofline(sess, dtype_name, key=key)
+        # The roofline describes the kernels at the headline launch size: one launch per layer over the
+        # whole per-GPU batch.  With --streams k the timed run splits that batch into k concurrent
+        # sub-batch graphs, whose launches overlap; the per-launch view is taken on the full-batch plan.
+        rsess, rkey = sess, key
+        if args.streams > 1:
+            rsess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=fp8, streams=1)
+            if args.fp8:
+                rsess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
+            rsess.load(blob_images(B, S, seed=1234 + rank).to(dev))
+            rsess()
+            rkey = key.replace(f"streams={args.streams}", "streams=1")
+        rf = roofline(rsess, dtype_name, key=rkey)
+        rf["plan"] = f"full-batch plan (bs {B}, one launch per layer); timed run on {args.streams} stream(s)"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.model, S, B, gpu_session=(model, fp8))
