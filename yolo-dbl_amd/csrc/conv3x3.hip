@@ -16,6 +16,8 @@
 // bank quads for any starting pixel, and the mixed-g lane groups of ds_read_b128
 // ({0-3,12-15,20-27}, ...) stay conflict-free; weights are [co/16][tap][g][co%16] for the same
 // reason.  Fused epilogue (bias, SiLU, residual add, channel-slice store) from conv_common.hpp.
+#include <stdlib.h>
+
 #include "conv_common.hpp"
 
 namespace ydbl {
@@ -185,7 +187,11 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   if (a.Cin % BK || a.Cin < 2 * BK || a.xcs % Vec<T>::N) return false;
   static const char* fth = getenv("YDBL_HALO_TH");  // A/B knob for scripts/conv_bench.py: force 4/8/16-row tiles
   const int force_th = fth && *fth ? atoi(fth) : 0;
-  if ((int64_t)a.P < 51200) return false;
+  const char* mp = getenv("YDBL_HALO_MINP");  // A/B knob (read per launch): smallest output-pixel count routed here
+  // 51200 output pixels (40^2 x 32) was the measured crossover at bs32; the bench's two bs16 sub-batch
+  // graphs put the 40^2 head convs at 25600, where the halo tile still wins (DBL-n bs32 on two streams
+  // 13.7 k -> 14.1 k img/s; 12800 loses again: 14.0 k)
+  if ((int64_t)a.P < (mp && *mp ? atoll(mp) : 25600)) return false;
   if (force_th == 4) return launch_halo<T, Q8, 1, 4>(a, s), true;
   if (force_th == 8) return launch_halo<T, Q8, 1, 8>(a, s), true;
   if (force_th == 16) return launch_halo<T, Q8, 1, 16>(a, s), true;
@@ -329,7 +335,9 @@ bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
   if (off || kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
   if (a.xcs % 8 || a.H != a.Ho || a.W != a.Wo || (int64_t)a.N * a.Ho * a.Wo >= (1LL << 31)) return false;
   if (a.Cin == 128 && a.Cout == 64) return launch_vw<128, 1, 4, 2>(a, 1, s), true;
-  if (a.Cin == 64 && a.Cout == 64 && a.P > 25600 && a.P <= 65536) return launch_vw<64, 2, 2, 4>(a, 1, s), true;
+  const char* vm = getenv("YDBL_VW_MINP");  // A/B knob (read per launch)
+  const int64_t vw_min = vm && *vm ? atoll(vm) : 25601;
+  if (a.Cin == 64 && a.Cout == 64 && a.P >= vw_min && a.P <= 65536) return launch_vw<64, 2, 2, 4>(a, 1, s), true;
   return false;
 }
 
