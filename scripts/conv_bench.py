@@ -2,6 +2,7 @@
 
     YDBL_NO_HALO=1 python scripts/conv_bench.py   # implicit-GEMM kernels only, for A/B
 """
+import os
 import sys
 from pathlib import Path
 
@@ -44,7 +45,7 @@ for idx, shp in enumerate(SHAPES):
     if sel and idx not in sel:
         continue
     ci, co, k, s, H = shp[:5]
-    B = shp[5] if len(shp) > 5 else 32
+    B = shp[5] if len(shp) > 5 else int(os.environ.get("YDBL_BENCH_B", 32))
     plan = Plan(torch.device("cuda"), torch.float16)
     x = plan.alloc(B, H, H, ci)
     x.torch().copy_(torch.randn(B, H, H, ci, dtype=torch.float16))

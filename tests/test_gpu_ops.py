@@ -169,9 +169,12 @@ def test_conv_tile(dtype, cin, cout, s, h, w, res):
     (32, 384, 64, 40, 40, None),      # DBL-n head Bottleneck cv1 (deep Cin, 40-wide map: ragged column tile)
     (2, 64, 96, 256, 256, None),      # 16-row tiles, partial second output-channel split
     (2, 320, 80, 160, 176, "add"),    # deep Cin (> 256) on a map large enough for the halo path
+    (16, 384, 64, 40, 40, None),      # bs16 sub-batch head conv: < 400 workgroups -> 32-channel slices
+    (16, 192, 48, 40, 40, "add"),     # 32-channel slices, partial second slice, residual
 ])
 def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
-    """3x3 stride-1 convs with Cin >= 64 on >= 51200 output pixels: the halo-tiled kernel (8/16-row tiles)."""
+    """3x3 stride-1 convs with Cin >= 64 on >= 25600 output pixels: the halo-tiled kernel (8/16-row tiles,
+    64- or 32-channel slices)."""
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense
 
@@ -180,7 +183,7 @@ def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
     wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
     b = torch.randn(cout)
     ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 1, 1))
-    assert n * h * w >= 51200
+    assert n * h * w >= 25600
     plan = _plan(dtype)
     xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
     ybuf = plan.alloc(n, h, w, cout + 8)

@@ -158,8 +158,16 @@ template <typename T, bool Q8, int S, int TH>
 static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
+  // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
+  // most CUs with one workgroup; 32-channel slices double the grid (conv_bench.py bs16: 384->64 @40^2
+  // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
+  const char* ev = getenv("YDBL_HALO_N2");  // A/B knob (read per launch)
+  const int64_t n2_below = ev && *ev ? atoll(ev) : 400;
   if (a.Cout <= 32) {
     conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
+  } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
+    const int cs = (int)cdiv(a.Cout, 32);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   } else {
     const int cs = (int)cdiv(a.Cout, 64);
     conv3x3_halo_kernel<T, S, TH, 4, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);

@@ -112,9 +112,11 @@ __global__ __launch_bounds__(256) void hg_proto_kernel(const float* __restrict__
     const float* c = ctxp + (int64_t)b * ns * K + i;
     float v = c[0];
     if (i < D) {
+#pragma unroll 8
       for (int k = 1; k < ns; ++k) v += c[(int64_t)k * K];
       v /= float(N);
     } else {
+#pragma unroll 8
       for (int k = 1; k < ns; ++k) v = fmaxf(v, c[(int64_t)k * K]);
     }
     sctx[i] = v;
@@ -154,6 +156,7 @@ __global__ __launch_bounds__(HG_LOGIT_TOK) void hg_logits_kernel(DView<const T> 
     float head[E];
 #pragma unroll
     for (int e = 0; e < E; ++e) tot[e] = head[e] = 0.f;
+#pragma unroll 4
     for (int d0 = 0; d0 < D; d0 += V) {
       float v[V];
       load_f<V>(row + d0, v);
@@ -227,8 +230,10 @@ __global__ __launch_bounds__(256) void hg_gather_kernel(DView<const T> x, const 
   if (threadIdx.x < E) {
     const int e = threadIdx.x;
     float m = -INFINITY;
+#pragma unroll 8
     for (int j = 0; j < nl; ++j) m = fmaxf(m, lstat[(((int64_t)b * nl + j) * E + e) * 2]);
     float sum = 0.f;
+#pragma unroll 8
     for (int j = 0; j < nl; ++j) {
       const float* st = lstat + (((int64_t)b * nl + j) * E + e) * 2;
       sum += st[1] * expf(st[0] - m);
@@ -298,6 +303,7 @@ __device__ __forceinline__ void hg_rows(const float* __restrict__ in, const floa
                                         int64_t gstride) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr int NW = HG_EDGE_THREADS / 64;
+#pragma unroll 4  // weight-row loads of 4 rows in flight together
   for (int d = wave; d < D; d += NW) {
     const float* wr = w + (int64_t)d * D;
     float s[E];
@@ -337,14 +343,17 @@ __global__ __launch_bounds__(HG_EDGE_THREADS) void hg_edge_kernel(const float* _
   for (int i = threadIdx.x; i < E * D; i += blockDim.x) {
     const float* p = hep + (int64_t)b * ns * E * D + i;
     float v = p[0];
+#pragma unroll 8  // the partial loads are independent: keep 8 in flight (same summation order)
     for (int k = 1; k < ns; ++k) v += p[(int64_t)k * E * D];
     sh[i] = v;
   }
   if (threadIdx.x < E) {
     const int e = threadIdx.x;
     float m = -INFINITY;
+#pragma unroll 8
     for (int j = 0; j < nl; ++j) m = fmaxf(m, lstat[(((int64_t)b * nl + j) * E + e) * 2]);
     float sum = 0.f;
+#pragma unroll 8
     for (int j = 0; j < nl; ++j) {
       const float* st = lstat + (((int64_t)b * nl + j) * E + e) * 2;
       sum += st[1] * expf(st[0] - m);

@@ -19,6 +19,8 @@
 // 16-lane pixel group: every ds_read_b128 is conflict-free.  The halo rows/cols of the first conv
 // (one extra row and column per tile, 6-8 % extra MFMA work) are recomputed instead of exchanged.
 // HBM traffic is the input once (+ halo re-reads, mostly L2 hits) and the output once.
+#include <stdlib.h>
+
 #include "conv_common.hpp"
 
 namespace ydbl {
@@ -302,6 +304,10 @@ extern "C" int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream) {
     return check_launch("ydbl_conv_stem2");
   };
   const bool v4 = d->w % 4 == 0 && (reinterpret_cast<uintptr_t>(d->x) & 15) == 0;
+  const char* ev = getenv("YDBL_STEM2_TH");  // A/B knob (read per launch): 4-row tiles
+  if (c0 == 8 && ev && atoi(ev) == 4)
+    return v4 ? go(stem2_kernel<8, 32, 4, true>, 32, 4, Stem2Cfg<8, 32, 4>::LDS)
+              : go(stem2_kernel<8, 32, 4, false>, 32, 4, Stem2Cfg<8, 32, 4>::LDS);
   if (c0 == 8)
     return v4 ? go(stem2_kernel<8, 32, 8, true>, 32, 8, Stem2Cfg<8, 32, 8>::LDS)
               : go(stem2_kernel<8, 32, 8, false>, 32, 8, Stem2Cfg<8, 32, 8>::LDS);
