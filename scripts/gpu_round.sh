@@ -13,5 +13,5 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -3 $OUT/smoke.log
 timeout -k 10 400 python bench.py > $OUT/bench.log 2>&1 || { echo bench failed; tail -30 $OUT/bench.log; exit 4; }
 tail -1 $OUT/bench.log
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo prof failed; tail -30 $OUT/prof.log; exit 5; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/prof -o run -- python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo prof failed; tail -30 $OUT/prof.log; exit 5; }
 find $OUT/prof -name '*stats*' | head

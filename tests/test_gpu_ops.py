@@ -971,15 +971,24 @@ def _rand_pred(n, nc, A, seed, ties=False):
     dict(nc=80, A=8400, conf=0.05, iou=0.7, multi=False, max_det=300),  # many classes: groups of 10 classes
     dict(nc=17, A=3000, conf=0.02, iou=0.6, multi=True, max_det=40),    # max_det cut across the merged lists
     dict(nc=9, A=2500, conf=0.01, iou=0.7, multi=True, max_nms=1500),   # max_nms: whole image in group 0
+    # pair-matrix path boundaries: n = 1024 (the largest it takes) and 1025 (sort + sweep)
+    dict(nc=1, A=1024, conf=0.0, iou=0.7, multi=False),
+    dict(nc=1, A=1025, conf=0.0, iou=0.7, multi=False),
+    dict(nc=3, A=1000, conf=0.0, iou=0.5, multi=False, max_nms=700),  # max_nms cut on the pair-matrix path
+    dict(nc=2, A=960, conf=0.0, iou=0.7, multi=False, max_det=5),     # max_det inside the first rank block
 ])
 @pytest.mark.parametrize("groups", ["1", "0"])
-def test_nms_bit_exact(case, groups, monkeypatch):
+@pytest.mark.parametrize("fast", ["1", "0"])
+def test_nms_bit_exact(case, groups, fast, monkeypatch):
     """groups "1": the class-split sweep (8 class-group workgroups per image + merge), "0": one workgroup
-    per image; both bit-exact against the restated torchvision semantics."""
+    per image; fast "1": images with <= 1024 candidates take the pair-matrix path (nms_pair_kernel + the
+    rank-order sweep), "0": sort + chunked sweep for every image.  All bit-exact against the restated
+    torchvision semantics."""
     from oracle.ops import non_max_suppression as ref_nms
     from ydbl.utils.ops import non_max_suppression
 
     monkeypatch.setenv("YDBL_NMS_GROUPS", groups)
+    monkeypatch.setenv("YDBL_NMS_FAST", fast)
     case = dict(case)
     nc, A = case.pop("nc"), case.pop("A")
     pred = _rand_pred(3, nc, A, seed=A + nc, ties=case.pop("ties", False))

@@ -11,6 +11,8 @@
 //          same as the reference's keep[:max_det] because keeps are produced in score order.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "common.hpp"
 
 #pragma clang fp contract(off)
@@ -30,6 +32,20 @@ struct DecodeArgs {
   float* cbox; float* cscore; int* ccls; int* cidx; int* ccount;
   int cap;
 };
+
+// Slot of this lane's candidate in image b's list: one atomic per wave (the first active lane adds the
+// wave's candidate count, the others take their rank among the active lanes).  Candidates cluster on
+// objects, so a wave often holds tens of them; per-lane atomics on the one counter serialize in L2.
+__device__ __forceinline__ int wave_slot(int* counter, bool want) {
+  const uint64_t m = __ballot(want);
+  if (!want) return -1;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  return base + __popcll(m & ((1ull << lane) - 1));
+}
 
 __device__ __forceinline__ bool class_ok(int j, const int* classes, int ncls) {
   if (!classes) return true;
@@ -65,9 +81,12 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
       e[k] = expf(v[k] - m);
       sum += e[k];
     }
+    // softmax weights as e * (1 / sum): one division per side instead of 16 (<= 1 ulp per weight, far
+    // inside the decode tolerance; the reference's DFL conv sums the 16 products in its own order anyway)
+    const float inv = 1.0f / sum;
     float acc = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) acc += float(k) * (e[k] / sum);
+    for (int k = 0; k < 16; ++k) acc += float(k) * (e[k] * inv);
     dist[s] = acc;
   }
   const float ax = float(gx) + 0.5f, ay = float(gy) + 0.5f, st = p.stride[l];
@@ -89,8 +108,8 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
     const float sc = 1.0f / (1.0f + expf(-float(cp[j])));
     if (p.yref) p.yref[((int64_t)b * (4 + p.nc) + 4 + j) * A + a] = sc;
     if (p.multi) {
-      if (sc > p.conf && class_ok(j, p.classes, p.ncls)) {
-        const int slot = atomicAdd(p.ccount + b, 1);
+      const int slot = wave_slot(p.ccount + b, sc > p.conf && class_ok(j, p.classes, p.ncls));
+      if (slot >= 0) {
         if (slot < p.cap) {
           const int64_t o = (int64_t)b * p.cap + slot;
           *reinterpret_cast<f32x4*>(p.cbox + o * 4) = f32x4{bx1, by1, bx2, by2};
@@ -102,8 +121,8 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
       bj = j;
     }
   }
-  if (!p.multi && best > p.conf && class_ok(bj, p.classes, p.ncls)) {
-    const int slot = atomicAdd(p.ccount + b, 1);
+  const int slot = p.multi ? -1 : wave_slot(p.ccount + b, best > p.conf && class_ok(bj, p.classes, p.ncls));
+  if (slot >= 0) {
     if (slot < p.cap) {
       const int64_t o = (int64_t)b * p.cap + slot;
       *reinterpret_cast<f32x4*>(p.cbox + o * 4) = f32x4{bx1, by1, bx2, by2};
@@ -126,8 +145,8 @@ __global__ __launch_bounds__(256) void pred_cand_kernel(ydbl_pred_cand_desc p) {
   for (int j = 0; j < p.nc; ++j) {
     const float sc = pr[(4 + j) * A];
     if (p.multi_label) {
-      if (sc > p.conf_thres && class_ok(j, p.classes, p.nclasses)) {
-        const int slot = atomicAdd(p.cand_count + b, 1);
+      const int slot = wave_slot(p.cand_count + b, sc > p.conf_thres && class_ok(j, p.classes, p.nclasses));
+      if (slot >= 0) {
         if (slot < p.cap) {
           const int64_t o = (int64_t)b * p.cap + slot;
           *reinterpret_cast<f32x4*>(p.cand_box + o * 4) = f32x4{bx1, by1, bx2, by2};
@@ -139,8 +158,9 @@ __global__ __launch_bounds__(256) void pred_cand_kernel(ydbl_pred_cand_desc p) {
       bj = j;
     }
   }
-  if (!p.multi_label && best > p.conf_thres && class_ok(bj, p.classes, p.nclasses)) {
-    const int slot = atomicAdd(p.cand_count + b, 1);
+  const int slot =
+      p.multi_label ? -1 : wave_slot(p.cand_count + b, best > p.conf_thres && class_ok(bj, p.classes, p.nclasses));
+  if (slot >= 0) {
     if (slot < p.cap) {
       const int64_t o = (int64_t)b * p.cap + slot;
       *reinterpret_cast<f32x4*>(p.cand_box + o * 4) = f32x4{bx1, by1, bx2, by2};
@@ -180,6 +200,7 @@ struct NmsArgs {
   uint64_t* gkeys; int* gvals; int L;  // global sort scratch (only when cap > NMS_SORT_LDS)
   int* gslot; uint64_t* gkey; int* gcount; int gk;  // per (image, class group) keep lists, gk entries each
   int cap;
+  uint64_t* fmask; int* frank; int frows; int fast;  // pair-matrix path (nms_pair_kernel), frows rows per image
   double thr; int max_det, max_nms; float off_scale;
   float clip_w, clip_h;
   float* out; int* out_count;
@@ -275,6 +296,112 @@ __device__ unsigned long long g_nms_stamps[16 * 4096];
 #define NMS_TICK(acc) do { } while (0)
 #endif
 
+// ---- pair-matrix path for images with n <= NMS_FAST candidates (the common case) --------------------
+// The greedy sweep of one image is serial, but everything it consumes is not: nms_pair_kernel spreads the
+// image's n x n candidate pairs over PW workgroups per image (one 64 x 64 block per wave) and writes, in
+// candidate (slot) order,
+//   fmask[b][i][w] bit s = IoU(box i, box 64w+s) > thr   (torchvision's decision, iou_gt; the IoU is
+//                                                         symmetric bit for bit, so row i is what box i
+//                                                         suppresses whichever of the two ranks first)
+//   frank[b][w][i]       = #{j in block w : key_j < key_i} (partial ranks; keys are unique)
+// and nms_kernel then only sums the ranks (rank = sort position, as the stable sort), stages the rows in
+// LDS and runs the sweep in rank order on one wave: a candidate is kept iff its bit in the running
+// removed mask is clear, and a kept candidate ORs its row into the mask.  Rows of candidates ranked
+// earlier get bits set too, which changes nothing: their decision is already made.
+constexpr int NMS_FAST = 1024;        // candidates per image on this path (mask rows staged in LDS: 128 KiB)
+constexpr int NMS_FW = NMS_FAST / 64;  // 64-bit words per mask row
+
+// LDS slot of word w of mask row c: the words of a row are XOR-permuted by the row's low bits, so that
+// 64 lanes reading the same word of 64 different rows (the rank-word build) spread over the banks, while
+// the 16 words of one row (the sweep's row reads) stay one conflict-free 128-byte line.
+__device__ __forceinline__ int mslot(int c, int w) { return c * NMS_FW + (w ^ (c & (NMS_FW - 1))); }
+
+__device__ __forceinline__ float rlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+constexpr int NMS_PAIR_MAXB = 1024;  // images per launch on the pair-matrix path (block offsets in LDS)
+constexpr int NMS_PAIR_WGS = 512;    // workgroups, each taking 64 x 64 blocks in turn
+
+// Persistent over all images' blocks: workgroups that would find an image with few candidates have no
+// idle launch cost (a (32 x images) grid spent ~20 us dispatching mostly empty workgroups), and the
+// blocks of a heavy image spread over the whole chip.
+__global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
+  __shared__ int s_pre[NMS_PAIR_MAXB + 1];  // s_pre[b] = blocks of images < b
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave == 0) {
+    int run = 0;
+    for (int b0 = 0; b0 < nimg; b0 += 64) {
+      const int bb = b0 + lane;
+      int cnt = 0;
+      if (bb < nimg) {
+        const int nn = min(p.ccount[bb], p.cap);
+        const int nbb = (nn + 63) >> 6;
+        cnt = nn <= NMS_FAST ? nbb * nbb : 0;
+      }
+      int incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      if (bb < nimg) s_pre[bb + 1] = run + incl;
+      run += __shfl(incl, 63);
+    }
+    if (lane == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+  __shared__ uint64_t s_bits[4][64];
+  __shared__ int s_cnt[4][64];
+  const int total = s_pre[nimg];
+  // a workgroup takes one 64 x 64 block at a time; wave w tests its rows against columns 16w .. 16w+15
+  for (int g = blockIdx.x; g < total; g += gridDim.x) {
+    int lo = 0, hi = nimg - 1;  // image b: s_pre[b] <= g < s_pre[b + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= g) lo = mid;
+      else hi = mid - 1;
+    }
+    const int b = lo;
+    const int n = min(p.ccount[b], p.cap);
+    const int nb = (n + 63) >> 6;
+    const int t = g - s_pre[b];
+    const int bi = t / nb, bj = t - bi * nb;
+    const float* cb = p.cbox + (int64_t)b * p.cap * 4;
+    const float* sc = p.cscore + (int64_t)b * p.cap;
+    const int* ix = p.cidx + (int64_t)b * p.cap;
+    const int* cc = p.ccls + (int64_t)b * p.cap;
+    auto box_of = [&](int i) -> f32x4 {  // the sweep's class-offset box (nms_kernel load_box)
+      const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)i * 4);
+      const float c = float(cc[i]) * p.off_scale;
+      return f32x4{v[0] + c, v[1] + c, v[2] + c, v[3] + c};
+    };
+    const int i = bi * 64 + lane, j = bj * 64 + 16 * wave + (lane & 15);
+    const int ic = min(i, n - 1), jc = min(j, n - 1);
+    const f32x4 xi = box_of(ic), xj = box_of(jc);
+    const float ai = (xi[2] - xi[0]) * (xi[3] - xi[1]);
+    const uint64_t ki = make_key(sc[ic], ix[ic]), kj = make_key(sc[jc], ix[jc]);
+    const uint32_t kjh = (uint32_t)(kj >> 32), kjl = (uint32_t)kj;
+    const int ns = min(16, n - bj * 64 - 16 * wave);  // this wave's columns (may be <= 0)
+    uint64_t bits = 0;
+    int below = 0;
+    for (int s = 0; s < ns; ++s) {
+      const f32x4 y = f32x4{rlane(xj[0], s), rlane(xj[1], s), rlane(xj[2], s), rlane(xj[3], s)};
+      const uint64_t k = ((uint64_t)__builtin_amdgcn_readlane(kjh, s) << 32) | __builtin_amdgcn_readlane(kjl, s);
+      below += k < ki;
+      if (iou_gt(xi, ai, y, p.thr)) bits |= 1ull << (16 * wave + s);
+    }
+    s_bits[wave][lane] = bits;
+    s_cnt[wave][lane] = below;
+    __syncthreads();
+    if (wave == 0 && i < n) {
+      p.fmask[((int64_t)b * p.frows + i) * NMS_FW + bj] = s_bits[0][lane] | s_bits[1][lane] | s_bits[2][lane] | s_bits[3][lane];
+      p.frank[((int64_t)b * NMS_FW + bj) * p.frows + i] = s_cnt[0][lane] + s_cnt[1][lane] + s_cnt[2][lane] + s_cnt[3][lane];
+    }
+    __syncthreads();
+  }
+}
+
 // GROUPS: the class-split form (non-agnostic NMS).  Boxes are offset by cls * max_wh, so boxes of
 // different classes never overlap and torchvision's greedy sweep is, class by class, independent: the
 // keep set of an image is the union of the keep sets of any partition of its classes, in (score, index)
@@ -285,10 +412,16 @@ __device__ unsigned long long g_nms_stamps[16 * 4096];
 template <bool GROUPS>
 __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   // LDS: sort keys (64 KB) are reused for the first 4096 sorted boxes after sorting.
-  __shared__ __align__(16) uint64_t s_keys[NMS_SORT_LDS];
-  __shared__ int s_vals[NMS_SORT_LDS];
-  __shared__ unsigned char removed[NMS_MAX_FLAGS];
+  // sort keys | sort slots | suppression flags, one buffer: the pair-matrix path stages its mask rows
+  // (NMS_FAST x NMS_FW words = 128 KiB) over all three
+  __shared__ __align__(16) unsigned char s_raw[NMS_SORT_LDS * 12 + NMS_MAX_FLAGS];
+  static_assert(NMS_FAST * NMS_FW * 8 <= NMS_SORT_LDS * 12 + NMS_MAX_FLAGS, "pair-matrix rows fit the sort buffers");
+  uint64_t* s_keys = reinterpret_cast<uint64_t*>(s_raw);
+  int* s_vals = reinterpret_cast<int*>(s_raw + NMS_SORT_LDS * 8);
+  unsigned char* removed = s_raw + NMS_SORT_LDS * 12;
   __shared__ int kept_slot[NMS_MAX_DET];
+  __shared__ int s_order[NMS_FAST];
+  __shared__ uint64_t s_dw[NMS_FAST];
   __shared__ int s_wsum[NMS_THREADS / 64];
   __shared__ f32x4 chunk_box[64];
   __shared__ float chunk_area[64];
@@ -303,272 +436,382 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   int n = min(p.ccount[b], p.cap);
   const float* sc = p.cscore + (int64_t)b * p.cap;
   const int* ix = p.cidx + (int64_t)b * p.cap;
-  bool listed = false;  // GROUPS: this group's (key, slot) list is already in s_keys / s_vals
-  if constexpr (GROUPS) {
-    const int64_t gi = (int64_t)b * NMS_GROUPS + grp;
-    if (n > p.max_nms || n > NMS_SORT_LDS) {  // whole image in group 0
-      if (grp != 0) {
-        if (threadIdx.x == 0) p.gcount[gi] = 0;
-        return;
-      }
-    } else {
-      const int* cc = p.ccls + (int64_t)b * p.cap;
-      if (threadIdx.x == 0) s_nk = 0;
-      __syncthreads();
-      for (int t = threadIdx.x; t < n; t += NMS_THREADS) {
-        if (cc[t] % NMS_GROUPS == grp) {  // list order is free: the sort key orders it
-          const int pos = atomicAdd(&s_nk, 1);
-          s_keys[pos] = make_key(sc[t], ix[t]);
-          s_vals[pos] = t;
-        }
-      }
-      __syncthreads();
-      n = s_nk;
-      __syncthreads();
-      listed = true;
-      if (n == 0) {
-        if (threadIdx.x == 0) p.gcount[gi] = 0;
+  if (p.fast && n <= NMS_FAST) {
+    // ---- pair-matrix path (nms_pair_kernel filled fmask / frank for this image)
+    if constexpr (GROUPS) {
+      if (grp != 0) {  // the whole image is group 0's
+        if (threadIdx.x == 0) p.gcount[(int64_t)b * NMS_GROUPS + grp] = 0;
         return;
       }
     }
-  }
-  // ---- 1. sort
-  const bool in_lds = n <= NMS_SORT_LDS;
-  int P = 64;
-  while (P < n) P <<= 1;
-  int* order;  // list position -> candidate slot
-  if (in_lds && P <= NMS_THREADS) {  // the common case: one candidate per thread, sorted in registers
-    const int t = threadIdx.x;
-    uint64_t key = ~0ull;
-    int val = -1;
-    if (t < n) {
-      key = listed ? s_keys[t] : make_key(sc[t], ix[t]);
-      val = listed ? s_vals[t] : t;
-    }
-    if (n > 1) reg_bitonic(key, val, P, s_keys + 2 * NMS_THREADS, s_vals + 2 * NMS_THREADS);
-    __syncthreads();
-    if (t < P) {
-      s_keys[t] = key;
-      s_vals[t] = val;
-    }
-    __syncthreads();
-    order = s_vals;
-  } else if (in_lds) {
-    for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
-      if (!listed || i >= n) {
-        s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
-        s_vals[i] = i < n ? i : -1;
-      }
-    }
-    __syncthreads();
-    if (n > 1) block_bitonic(s_keys, s_vals, P);
-    order = s_vals;
-  } else {
-    uint64_t* gk = p.gkeys + (int64_t)b * p.L;
-    int* gv = p.gvals + (int64_t)b * p.L;
-    for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
-      gk[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
-      gv[i] = i < n ? i : -1;
-    }
-    __syncthreads();
-    block_bitonic(gk, gv, P);
-    order = gv;
-  }
-  const int m = min(n, p.max_nms);
-  NMS_STAMP(1, __builtin_amdgcn_s_memrealtime());
-  NMS_STAMP(6, (unsigned long long)m);
-  // ---- stage boxes (class-offset) of the first LDS_BOXES sorted candidates; flags
-  const float* cb = p.cbox + (int64_t)b * p.cap * 4;
-  const int* cc = p.ccls + (int64_t)b * p.cap;
-  auto load_box = [&](int i) -> f32x4 {
-    const int slot = order[i];
-    const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)slot * 4);
-    const float c = float(cc[slot]) * p.off_scale;  // boxes + cls * max_wh (0 if agnostic)
-    return f32x4{v[0] + c, v[1] + c, v[2] + c, v[3] + c};
-  };
-  // s_box aliases s_keys: read every box first, then write (order[] = s_vals is separate)
-  f32x4 mine[LDS_BOXES / NMS_THREADS];
-#pragma unroll
-  for (int r = 0; r < LDS_BOXES / NMS_THREADS; ++r) {
-    const int i = threadIdx.x + r * NMS_THREADS;
-    if (i < m) mine[r] = load_box(i);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < LDS_BOXES / NMS_THREADS; ++r) {
-    const int i = threadIdx.x + r * NMS_THREADS;
-    if (i < m) s_box[i] = mine[r];
-  }
-  for (int i = threadIdx.x; i < m; i += NMS_THREADS) removed[i] = 0;
-  if (threadIdx.x == 0) s_nk = 0;
-  __syncthreads();
-  auto box_at = [&](int i) -> f32x4 { return i < LDS_BOXES ? s_box[i] : load_box(i); };
-
-  // ---- 3. chunked greedy sweep.  With the sorted list in LDS (n <= NMS_SORT_LDS) the list is
-  // compacted after every chunk: the next chunk is always the 64 best boxes still alive, so the
-  // number of rounds follows the boxes that survive, not the candidate count.  Above that the chunk
-  // walks the sorted positions and skips suppressed ones by flag.
-  const bool compact = in_lds;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;  // 16 waves
-  int m_cur = m;
-  NMS_STAMP(2, __builtin_amdgcn_s_memrealtime());
-  int rounds = 0;
-#ifdef YDBL_NMS_STAMPS
-  unsigned long long t_last = __builtin_amdgcn_s_memrealtime(), ta = 0, tb = 0, tc = 0, td = 0;
-#endif
-  for (int c0 = 0; c0 < m_cur;) {
-    ++rounds;
-    const int nk0 = s_nk;
-    if (nk0 >= p.max_det) break;
-    // (a) intra-chunk suppression masks: wave w tests columns c0+4w..c0+4w+3 against row c0+lane
-    const int i = c0 + lane;
-    const bool live = i < m_cur && !removed[i];
-    f32x4 bi = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int m = min(n, p.max_nms);  // the reference's argsort(descending)[:max_nms]
+    const int nb = (n + 63) >> 6;
+    const int* rpart = p.frank + (int64_t)b * NMS_FW * p.frows;
+    // every global load of this thread is issued before the first one is used (fixed trip counts)
+    static_assert(NMS_FAST == NMS_THREADS, "one candidate per thread");
     {
-      unsigned bits = 0;
-      if (live) {
-        bi = box_at(i);
-        const float ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+      const int i = threadIdx.x;
+      int part[NMS_FW];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int j = c0 + 4 * wave + q;
-          if (j > i && j < m_cur && !removed[j] && iou_gt(bi, ai, box_at(j), p.thr)) bits |= 1u << q;
-        }
+      for (int w = 0; w < NMS_FW; ++w) part[w] = i < n && w < nb ? rpart[w * p.frows + i] : 0;
+      int r = 0;
+#pragma unroll
+      for (int w = 0; w < NMS_FW; ++w) r += part[w];
+      if (i < n && r < m) s_order[r] = i;
+    }
+    uint64_t* smask = reinterpret_cast<uint64_t*>(s_raw);  // [n][NMS_FW]
+    {
+      const uint64_t* gm = p.fmask + (int64_t)b * p.frows * NMS_FW;
+      uint64_t v[NMS_FW];
+#pragma unroll
+      for (int k = 0; k < NMS_FW; ++k) {
+        const int e = threadIdx.x + k * NMS_THREADS;
+        v[k] = e < n * NMS_FW && (e & (NMS_FW - 1)) < nb ? gm[e] : 0ull;
       }
-      cmask[lane][wave] = (unsigned char)bits;
+#pragma unroll
+      for (int k = 0; k < NMS_FW; ++k) {
+        const int e = threadIdx.x + k * NMS_THREADS;
+        if (e < n * NMS_FW) smask[mslot(e >> 4, e & (NMS_FW - 1))] = v[k];
+      }
     }
     __syncthreads();
-    NMS_TICK(ta);
-    // (b) wave 0 resolves the chunk on scalar registers only (find-first-set, readlane of the kept
-    // row's mask, and-not), then every lane places itself by the rank of its bit in the kept mask
-    if (wave == 0) {
-      uint64_t rm = 0;
-#pragma unroll
-      for (int w = 0; w < 16; ++w) rm |= (uint64_t)cmask[lane][w] << (4 * w);
-      uint64_t M = __ballot(live), K = 0;
-      int nk = nk0;
-      while (M && nk < p.max_det) {
-        const int t = __ffsll((long long)M) - 1;
-        const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rm, t);
-        const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(rm >> 32), t);
-        K |= 1ull << t;
-        M &= ~((((uint64_t)hi << 32) | lo) | (1ull << t));
-        ++nk;
+    NMS_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    NMS_STAMP(2, __builtin_amdgcn_s_memrealtime());
+    NMS_STAMP(6, (unsigned long long)m);
+    // within-block suppression words in rank space: s_dw[r] bit s = row of rank r suppresses rank
+    // 64*(r/64) + s, for s > r%64 (wave w builds block w: the column candidates are wave-uniform)
+    // (branch-free body: the 64 row reads of a lane are issued back to back)
+    if ((int)(threadIdx.x & ~63) < m) {
+      const int r = threadIdx.x, k0 = r & ~63, rl = r & 63;
+      const int cr = r < m ? s_order[r] : 0;  // lane rl holds the candidate of rank k0 + rl (this wave's block)
+      const int send = min(64, m - k0);
+      uint64_t dw = 0;
+#pragma unroll 8
+      for (int q = 0; q < 64; ++q) {
+        const int cq = __builtin_amdgcn_readlane(cr, q);
+        const uint64_t bit = (smask[mslot(cr, (cq >> 6) & (NMS_FW - 1))] >> (cq & 63)) & 1ull;
+        dw |= (q > rl && q < send) ? bit << q : 0ull;
       }
-      if ((K >> lane) & 1) {
-        const int rank = __popcll(K & ((1ull << lane) - 1));
-        kept_slot[nk0 + rank] = order[i];
-        chunk_box[rank] = bi;
-        chunk_area[rank] = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+      if (r < m) s_dw[r] = dw;
+    }
+    __syncthreads();
+    NMS_STAMP(4, __builtin_amdgcn_s_memrealtime());
+    if (threadIdx.x < 64) {  // one wave sweeps the rank blocks in order
+      const int lane = threadIdx.x;
+      uint64_t rem = 0;  // lane w < nb: removed flags of candidates 64w .. 64w+63
+      int nk = 0;
+      for (int t0 = 0; t0 < m && nk < p.max_det; t0 += 64) {
+        const bool valid = t0 + lane < m;
+        const int myc = valid ? s_order[t0 + lane] : 0;
+        const uint64_t dw = valid ? s_dw[t0 + lane] : 0ull;
+        // alive = not removed by a kept candidate of an earlier block
+        const int wsrc = myc >> 6;
+        const uint32_t rlo = __shfl((uint32_t)rem, wsrc), rhi = __shfl((uint32_t)(rem >> 32), wsrc);
+        const uint64_t rw = ((uint64_t)rhi << 32) | rlo;
+        uint64_t M = __ballot(valid && !((rw >> (myc & 63)) & 1)), K = 0;
+        const int nk0 = nk;
+        // greedy inside the block on scalar registers: keep the first live rank, drop what it suppresses
+        while (M && nk < p.max_det) {
+          const int t = __ffsll((long long)M) - 1;
+          const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)dw, t);
+          const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(dw >> 32), t);
+          K |= 1ull << t;
+          M &= ~((((uint64_t)hi << 32) | lo) | (1ull << t));
+          ++nk;
+        }
+        if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = myc;
+        // the kept candidates' rows join the removed flags (8 row reads in flight at a time)
+        // (branch-free: all 8 reads are issued before the first OR)
+        while (K) {
+          int c[8];
+          bool ok[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int t = __ffsll((long long)K) - 1;  // -1 once K is empty
+            K &= K - 1;
+            ok[q] = t >= 0;
+            c[q] = __builtin_amdgcn_readlane(myc, t & 63);
+          }
+          uint64_t row[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) row[q] = smask[mslot(c[q], lane & (NMS_FW - 1))];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) rem |= ok[q] && lane < nb ? row[q] : 0ull;
+        }
       }
       if (lane == 0) s_nk = nk;
     }
     __syncthreads();
-    const int ck = s_nk - nk0;
-    if (s_nk >= p.max_det) break;
-    NMS_TICK(tb);
-    // (c) suppress every later box against the chunk's kept boxes (all of which precede it).  The
-    // (box, kept box) pairs are spread over the whole workgroup: G thread groups (G in 1..16) each test
-    // every box against every G-th kept box, any hit sets the flag; G minimises the per-thread test
-    // count ceil(R G / 1024) * ceil(ck / G) (R later boxes, ck kept boxes).
-    const int R = m_cur - (c0 + 64);
-    if (R > 0 && ck > 0) {
-      int G = 1, best = 1 << 30;
-      for (int g = 1; g <= 16; g <<= 1) {
-        const int cost = ((R * g + NMS_THREADS - 1) / NMS_THREADS) * ((ck + g - 1) / g);
-        if (g <= ck && cost < best) {
-          best = cost;
-          G = g;
+    NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
+    NMS_STAMP(5, 0ull);
+  } else {
+    bool listed = false;  // GROUPS: this group's (key, slot) list is already in s_keys / s_vals
+    if constexpr (GROUPS) {
+      const int64_t gi = (int64_t)b * NMS_GROUPS + grp;
+      if (n > p.max_nms || n > NMS_SORT_LDS) {  // whole image in group 0
+        if (grp != 0) {
+          if (threadIdx.x == 0) p.gcount[gi] = 0;
+          return;
         }
-      }
-      const int TS = NMS_THREADS / G;
-      const int tg = threadIdx.x / TS, r = threadIdx.x - tg * TS;
-      if (tg < G) {
-        for (int j = c0 + 64 + r; j < m_cur; j += TS) {
-          if (removed[j]) continue;
-          const f32x4 bj = box_at(j);
-          // kept boxes in batches of 8: the 8 broadcast LDS reads are in flight together and the tests
-          // are independent (any hit suppresses; testing past the first hit changes nothing)
-          bool sup = false;
-          for (int q0 = tg; q0 < ck && !sup; q0 += 8 * G) {
-            f32x4 bq[8];
-            float aq[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              const int q = min(q0 + u * G, ck - 1);
-              bq[u] = chunk_box[q];
-              aq[u] = chunk_area[q];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-              if (q0 + u * G < ck) sup |= iou_gt(bq[u], aq[u], bj, p.thr);
+      } else {
+        const int* cc = p.ccls + (int64_t)b * p.cap;
+        if (threadIdx.x == 0) s_nk = 0;
+        __syncthreads();
+        for (int t = threadIdx.x; t < n; t += NMS_THREADS) {
+          if (cc[t] % NMS_GROUPS == grp) {  // list order is free: the sort key orders it
+            const int pos = atomicAdd(&s_nk, 1);
+            s_keys[pos] = make_key(sc[t], ix[t]);
+            s_vals[pos] = t;
           }
-          if (sup) removed[j] = 1;
+        }
+        __syncthreads();
+        n = s_nk;
+        __syncthreads();
+        listed = true;
+        if (n == 0) {
+          if (threadIdx.x == 0) p.gcount[gi] = 0;
+          return;
         }
       }
     }
-    __syncthreads();
-    NMS_TICK(tc);
-    if (!compact) {
-      c0 += 64;
-      continue;
-    }
-    // (d) compaction (c0 == 0): survivors of positions [64, m_cur) move to [0, R') in order.  Each
-    // thread owns a contiguous run of E <= 8 positions held in registers (all reads before the
-    // barrier, all writes after it); a wave scan + per-wave totals give the destinations.
-    if (R <= 0) break;
-    constexpr int EMAX = NMS_SORT_LDS / NMS_THREADS;
-    const int E = (R + NMS_THREADS - 1) / NMS_THREADS;
-    f32x4 kb[EMAX];
-    int ks[EMAX];
-    bool kv[EMAX];
-    int cnt = 0;
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-      const int pos = 64 + threadIdx.x * E + e;
-      kv[e] = e < E && pos < m_cur && !removed[pos];
-      if (kv[e]) {
-        kb[e] = box_at(pos);
-        ks[e] = order[pos];
-        ++cnt;
+    // ---- 1. sort
+    const bool in_lds = n <= NMS_SORT_LDS;
+    int P = 64;
+    while (P < n) P <<= 1;
+    int* order;  // list position -> candidate slot
+    if (in_lds && P <= NMS_THREADS) {  // the common case: one candidate per thread, sorted in registers
+      const int t = threadIdx.x;
+      uint64_t key = ~0ull;
+      int val = -1;
+      if (t < n) {
+        key = listed ? s_keys[t] : make_key(sc[t], ix[t]);
+        val = listed ? s_vals[t] : t;
       }
-    }
-    int incl = cnt;  // inclusive scan over the wave
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int v = __shfl_up(incl, d);
-      if (lane >= d) incl += v;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    __syncthreads();
-    int off = incl - cnt, total = 0;
-#pragma unroll
-    for (int w = 0; w < NMS_THREADS / 64; ++w) {
-      const int t = s_wsum[w];
-      off += w < wave ? t : 0;
-      total += t;
-    }
-    int dst = off;
-#pragma unroll
-    for (int e = 0; e < EMAX; ++e) {
-      if (kv[e]) {
-        order[dst] = ks[e];
-        if (dst < LDS_BOXES) s_box[dst] = kb[e];
-        removed[dst] = 0;
-        ++dst;
+      if (n > 1) reg_bitonic(key, val, P, s_keys + 2 * NMS_THREADS, s_vals + 2 * NMS_THREADS);
+      __syncthreads();
+      if (t < P) {
+        s_keys[t] = key;
+        s_vals[t] = val;
       }
+      __syncthreads();
+      order = s_vals;
+    } else if (in_lds) {
+      for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
+        if (!listed || i >= n) {
+          s_keys[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+          s_vals[i] = i < n ? i : -1;
+        }
+      }
+      __syncthreads();
+      if (n > 1) block_bitonic(s_keys, s_vals, P);
+      order = s_vals;
+    } else {
+      uint64_t* gk = p.gkeys + (int64_t)b * p.L;
+      int* gv = p.gvals + (int64_t)b * p.L;
+      for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
+        gk[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+        gv[i] = i < n ? i : -1;
+      }
+      __syncthreads();
+      block_bitonic(gk, gv, P);
+      order = gv;
     }
-    m_cur = total;
-    NMS_TICK(td);
+    const int m = min(n, p.max_nms);
+    NMS_STAMP(1, __builtin_amdgcn_s_memrealtime());
+    NMS_STAMP(6, (unsigned long long)m);
+    // ---- stage boxes (class-offset) of the first LDS_BOXES sorted candidates; flags
+    const float* cb = p.cbox + (int64_t)b * p.cap * 4;
+    const int* cc = p.ccls + (int64_t)b * p.cap;
+    auto load_box = [&](int i) -> f32x4 {
+      const int slot = order[i];
+      const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)slot * 4);
+      const float c = float(cc[slot]) * p.off_scale;  // boxes + cls * max_wh (0 if agnostic)
+      return f32x4{v[0] + c, v[1] + c, v[2] + c, v[3] + c};
+    };
+    // s_box aliases s_keys: read every box first, then write (order[] = s_vals is separate)
+    f32x4 mine[LDS_BOXES / NMS_THREADS];
+#pragma unroll
+    for (int r = 0; r < LDS_BOXES / NMS_THREADS; ++r) {
+      const int i = threadIdx.x + r * NMS_THREADS;
+      if (i < m) mine[r] = load_box(i);
+    }
     __syncthreads();
-  }
-  __syncthreads();
-  NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
-  NMS_STAMP(5, (unsigned long long)rounds);
+#pragma unroll
+    for (int r = 0; r < LDS_BOXES / NMS_THREADS; ++r) {
+      const int i = threadIdx.x + r * NMS_THREADS;
+      if (i < m) s_box[i] = mine[r];
+    }
+    for (int i = threadIdx.x; i < m; i += NMS_THREADS) removed[i] = 0;
+    if (threadIdx.x == 0) s_nk = 0;
+    __syncthreads();
+    auto box_at = [&](int i) -> f32x4 { return i < LDS_BOXES ? s_box[i] : load_box(i); };
+
+    // ---- 3. chunked greedy sweep.  With the sorted list in LDS (n <= NMS_SORT_LDS) the list is
+    // compacted after every chunk: the next chunk is always the 64 best boxes still alive, so the
+    // number of rounds follows the boxes that survive, not the candidate count.  Above that the chunk
+    // walks the sorted positions and skips suppressed ones by flag.
+    const bool compact = in_lds;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;  // 16 waves
+    int m_cur = m;
+    NMS_STAMP(2, __builtin_amdgcn_s_memrealtime());
+    int rounds = 0;
 #ifdef YDBL_NMS_STAMPS
-  NMS_STAMP(7, ta); NMS_STAMP(8, tb); NMS_STAMP(9, tc); NMS_STAMP(10, td);
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime(), ta = 0, tb = 0, tc = 0, td = 0;
 #endif
+    for (int c0 = 0; c0 < m_cur;) {
+      ++rounds;
+      const int nk0 = s_nk;
+      if (nk0 >= p.max_det) break;
+      // (a) intra-chunk suppression masks: wave w tests columns c0+4w..c0+4w+3 against row c0+lane
+      const int i = c0 + lane;
+      const bool live = i < m_cur && !removed[i];
+      f32x4 bi = f32x4{0.f, 0.f, 0.f, 0.f};
+      {
+        unsigned bits = 0;
+        if (live) {
+          bi = box_at(i);
+          const float ai = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j = c0 + 4 * wave + q;
+            if (j > i && j < m_cur && !removed[j] && iou_gt(bi, ai, box_at(j), p.thr)) bits |= 1u << q;
+          }
+        }
+        cmask[lane][wave] = (unsigned char)bits;
+      }
+      __syncthreads();
+      NMS_TICK(ta);
+      // (b) wave 0 resolves the chunk on scalar registers only (find-first-set, readlane of the kept
+      // row's mask, and-not), then every lane places itself by the rank of its bit in the kept mask
+      if (wave == 0) {
+        uint64_t rm = 0;
+#pragma unroll
+        for (int w = 0; w < 16; ++w) rm |= (uint64_t)cmask[lane][w] << (4 * w);
+        uint64_t M = __ballot(live), K = 0;
+        int nk = nk0;
+        while (M && nk < p.max_det) {
+          const int t = __ffsll((long long)M) - 1;
+          const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)rm, t);
+          const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(rm >> 32), t);
+          K |= 1ull << t;
+          M &= ~((((uint64_t)hi << 32) | lo) | (1ull << t));
+          ++nk;
+        }
+        if ((K >> lane) & 1) {
+          const int rank = __popcll(K & ((1ull << lane) - 1));
+          kept_slot[nk0 + rank] = order[i];
+          chunk_box[rank] = bi;
+          chunk_area[rank] = (bi[2] - bi[0]) * (bi[3] - bi[1]);
+        }
+        if (lane == 0) s_nk = nk;
+      }
+      __syncthreads();
+      const int ck = s_nk - nk0;
+      if (s_nk >= p.max_det) break;
+      NMS_TICK(tb);
+      // (c) suppress every later box against the chunk's kept boxes (all of which precede it).  The
+      // (box, kept box) pairs are spread over the whole workgroup: G thread groups (G in 1..16) each test
+      // every box against every G-th kept box, any hit sets the flag; G minimises the per-thread test
+      // count ceil(R G / 1024) * ceil(ck / G) (R later boxes, ck kept boxes).
+      const int R = m_cur - (c0 + 64);
+      if (R > 0 && ck > 0) {
+        int G = 1, best = 1 << 30;
+        for (int g = 1; g <= 16; g <<= 1) {
+          const int cost = ((R * g + NMS_THREADS - 1) / NMS_THREADS) * ((ck + g - 1) / g);
+          if (g <= ck && cost < best) {
+            best = cost;
+            G = g;
+          }
+        }
+        const int TS = NMS_THREADS / G;
+        const int tg = threadIdx.x / TS, r = threadIdx.x - tg * TS;
+        if (tg < G) {
+          for (int j = c0 + 64 + r; j < m_cur; j += TS) {
+            if (removed[j]) continue;
+            const f32x4 bj = box_at(j);
+            // kept boxes in batches of 8: the 8 broadcast LDS reads are in flight together and the tests
+            // are independent (any hit suppresses; testing past the first hit changes nothing)
+            bool sup = false;
+            for (int q0 = tg; q0 < ck && !sup; q0 += 8 * G) {
+              f32x4 bq[8];
+              float aq[8];
+#pragma unroll
+              for (int u = 0; u < 8; ++u) {
+                const int q = min(q0 + u * G, ck - 1);
+                bq[u] = chunk_box[q];
+                aq[u] = chunk_area[q];
+              }
+#pragma unroll
+              for (int u = 0; u < 8; ++u)
+                if (q0 + u * G < ck) sup |= iou_gt(bq[u], aq[u], bj, p.thr);
+            }
+            if (sup) removed[j] = 1;
+          }
+        }
+      }
+      __syncthreads();
+      NMS_TICK(tc);
+      if (!compact) {
+        c0 += 64;
+        continue;
+      }
+      // (d) compaction (c0 == 0): survivors of positions [64, m_cur) move to [0, R') in order.  Each
+      // thread owns a contiguous run of E <= 8 positions held in registers (all reads before the
+      // barrier, all writes after it); a wave scan + per-wave totals give the destinations.
+      if (R <= 0) break;
+      constexpr int EMAX = NMS_SORT_LDS / NMS_THREADS;
+      const int E = (R + NMS_THREADS - 1) / NMS_THREADS;
+      f32x4 kb[EMAX];
+      int ks[EMAX];
+      bool kv[EMAX];
+      int cnt = 0;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        const int pos = 64 + threadIdx.x * E + e;
+        kv[e] = e < E && pos < m_cur && !removed[pos];
+        if (kv[e]) {
+          kb[e] = box_at(pos);
+          ks[e] = order[pos];
+          ++cnt;
+        }
+      }
+      int incl = cnt;  // inclusive scan over the wave
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      if (lane == 63) s_wsum[wave] = incl;
+      __syncthreads();
+      int off = incl - cnt, total = 0;
+#pragma unroll
+      for (int w = 0; w < NMS_THREADS / 64; ++w) {
+        const int t = s_wsum[w];
+        off += w < wave ? t : 0;
+        total += t;
+      }
+      int dst = off;
+#pragma unroll
+      for (int e = 0; e < EMAX; ++e) {
+        if (kv[e]) {
+          order[dst] = ks[e];
+          if (dst < LDS_BOXES) s_box[dst] = kb[e];
+          removed[dst] = 0;
+          ++dst;
+        }
+      }
+      m_cur = total;
+      NMS_TICK(td);
+      __syncthreads();
+    }
+    __syncthreads();
+    NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
+    NMS_STAMP(5, (unsigned long long)rounds);
+#ifdef YDBL_NMS_STAMPS
+    NMS_STAMP(7, ta); NMS_STAMP(8, tb); NMS_STAMP(9, tc); NMS_STAMP(10, td);
+#endif
+  }
   const int kept = min(s_nk, p.max_det);
   if constexpr (GROUPS) {  // this group's keep list for nms_merge_kernel
     const int64_t gi = (int64_t)b * NMS_GROUPS + grp;
@@ -750,8 +993,11 @@ extern "C" int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream) 
 }
 
 // [global sort keys n*L x 8 B][sort slots n*L x 4 B][group keys n*G*gk x 8 B][group slots x 4 B][counts n*G x 4 B]
+// [pad to 8 B][pair-matrix rows n*R*NMS_FW x 8 B][partial ranks n*NMS_FW*R x 4 B]
 static int64_t nms_sort_len(int32_t cap) { return cap <= NMS_SORT_LDS ? 0 : next_pow2(cap); }
 static int32_t nms_group_len(int32_t cap) { return cap < NMS_MAX_DET ? cap : NMS_MAX_DET; }
+// rows per image of the pair-matrix workspace: candidates up to NMS_FAST, in whole 64-row blocks
+static int32_t nms_fast_rows(int32_t cap) { return (std::min(cap, NMS_FAST) + 63) / 64 * 64; }
 
 #ifdef YDBL_NMS_STAMPS
 extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
@@ -762,8 +1008,9 @@ extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
 extern "C" int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms) {
   (void)max_nms;
   if (n < 1 || cap < 1) return 16;
-  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap);
-  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 16;
+  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap), R = nms_fast_rows(cap);
+  // + pair-matrix rows (u64 x NMS_FW) and partial ranks (int x NMS_FW) per candidate row, 8-byte aligned
+  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 8 + (int64_t)n * R * NMS_FW * 12 + 16;
 }
 
 extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
@@ -791,6 +1038,12 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   a.off_scale = d->agnostic ? 0.f : d->max_wh;
   a.clip_w = d->clip_w; a.clip_h = d->clip_h;
   a.out = d->out; a.out_count = d->out_count;
+  a.frows = nms_fast_rows(d->cap);
+  a.fmask = reinterpret_cast<uint64_t*>(a.gcount + (int64_t)d->n * NMS_GROUPS + ((int64_t)d->n * NMS_GROUPS & 1));
+  a.frank = reinterpret_cast<int*>(a.fmask + (int64_t)d->n * a.frows * NMS_FW);
+  const char* fe = getenv("YDBL_NMS_FAST");  // A/B switch (read per launch: tests): 0 = sort + chunked sweep only
+  a.fast = !(fe && *fe == '0') && d->n <= NMS_PAIR_MAXB;
+  if (a.fast) nms_pair_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
   // class-split sweep + merge (non-agnostic); the one-workgroup-per-image form for agnostic NMS or on request
   const char* ev = getenv("YDBL_NMS_GROUPS");  // A/B switch (read per launch: tests): 0 = one workgroup per image
   if (d->agnostic || (ev && *ev == '0')) {
