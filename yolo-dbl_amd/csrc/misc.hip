@@ -193,11 +193,11 @@ constexpr int DWP_HWMAX = 512;
 // bs32: this plain form, 36-38 us for both LSK depthwise convs, beat tap-unrolled variants with
 // 2-4 independent pixels in flight, 42-53 us: their LDS reads and code size cost more than the ILP
 // they bought.)
-template <typename T, int K, int D, int CV>
+template <typename T, int K, int D, int CV, int NT>
 __device__ __forceinline__ void dw_pair_phase(const typename Vec<T>::type* src, const f32x4* wts, const float* bias,
                                               int pad, int act, DView<T> out, typename Vec<T>::type* keep, int b,
                                               int cc, int cv, int pl, int H, int W) {
-  constexpr int V = Vec<T>::N, LANES = 256 / CV;
+  constexpr int V = Vec<T>::N, LANES = NT / CV;
   using vec = typename Vec<T>::type;
   float bv[V];
 #pragma unroll
@@ -238,8 +238,11 @@ __device__ __forceinline__ void dw_pair_phase(const typename Vec<T>::type* src, 
   }
 }
 
-template <typename T, int K0, int D0, int K1, int D1, int CV>
-__global__ __launch_bounds__(256) void dw_pair_kernel(DView<const T> x, DView<T> y0, DView<T> y1,
+// NT = 1024 threads: a pixel's taps are a chain of dependent LDS reads, and at one workgroup per CU (16
+// images x 256 channels / 16 = 256 workgroups) four waves per SIMD hide that latency where one did not
+// (DBL-n bs16 LSK pair 39.5 -> 20.9 us, bit-identical).
+template <typename T, int K0, int D0, int K1, int D1, int CV, int NT>
+__global__ __launch_bounds__(NT) void dw_pair_kernel(DView<const T> x, DView<T> y0, DView<T> y1,
                                                       const float* __restrict__ w0, const float* __restrict__ b0,
                                                       const float* __restrict__ w1, const float* __restrict__ b1,
                                                       int pad0, int pad1, int act0, int act1) {
@@ -251,31 +254,31 @@ __global__ __launch_bounds__(256) void dw_pair_kernel(DView<const T> x, DView<T>
   const int cgroups = C / (CV * V);
   const int b = blockIdx.x / cgroups, c0 = (blockIdx.x % cgroups) * CV * V;
   {  // all of a thread's map loads in flight before the first LDS store
-    constexpr int IT = DWP_HWMAX * CV / 256;
+    constexpr int IT = (DWP_HWMAX * CV + NT - 1) / NT;
     vec tmp[IT];
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
-      const int i = threadIdx.x + u * 256, cv = i % CV, px = min(i / CV, HW - 1);
+      const int i = threadIdx.x + u * NT, cv = i % CV, px = min(i / CV, HW - 1);
       tmp[u] = vload(x.at(b, px / W, px % W) + c0 + cv * V);
     }
 #pragma unroll
     for (int u = 0; u < IT; ++u)
-      if (threadIdx.x + u * 256 < HW * CV) tx[threadIdx.x + u * 256] = tmp[u];
+      if (threadIdx.x + u * NT < HW * CV) tx[threadIdx.x + u * NT] = tmp[u];
   }
-  for (int i = threadIdx.x; i < K0 * K0 * CV * V / 4; i += 256) {
+  for (int i = threadIdx.x; i < K0 * K0 * CV * V / 4; i += NT) {
     const int tap = i / (CV * V / 4), q = i % (CV * V / 4);
     ws0[i] = *reinterpret_cast<const f32x4*>(w0 + tap * C + c0 + 4 * q);
   }
-  for (int i = threadIdx.x; i < K1 * K1 * CV * V / 4; i += 256) {
+  for (int i = threadIdx.x; i < K1 * K1 * CV * V / 4; i += NT) {
     const int tap = i / (CV * V / 4), q = i % (CV * V / 4);
     ws1[i] = *reinterpret_cast<const f32x4*>(w1 + tap * C + c0 + 4 * q);
   }
   __syncthreads();
   const int cv = threadIdx.x % CV, pl = threadIdx.x / CV;
   const int cc = c0 + cv * V;
-  dw_pair_phase<T, K0, D0, CV>(tx, ws0, b0, pad0, act0, y0, ta, b, cc, cv, pl, H, W);
+  dw_pair_phase<T, K0, D0, CV, NT>(tx, ws0, b0, pad0, act0, y0, ta, b, cc, cv, pl, H, W);
   __syncthreads();
-  dw_pair_phase<T, K1, D1, CV>(ta, ws1, b1, pad1, act1, y1, nullptr, b, cc, cv, pl, H, W);
+  dw_pair_phase<T, K1, D1, CV, NT>(ta, ws1, b1, pad1, act1, y1, nullptr, b, cc, cv, pl, H, W);
 }
 
 // ------------------------------------------------------------------ input NCHW fp32 -> NHWC
@@ -580,12 +583,13 @@ extern "C" int ydbl_dwconv2d_pair_nhwc(const ydbl_dwconv_desc* d0, const ydbl_dw
   }
   hipStream_t s = as_stream(stream);
   const unsigned blocks = (unsigned)(d0->y.n * (d0->y.c / (CV * V)));
+  constexpr int NT = 1024;
   if (d0->x.dtype == YDBL_F16)
-    dw_pair_kernel<_Float16, 5, 1, 7, 3, CV><<<blocks, 256, 0, s>>>(
+    dw_pair_kernel<_Float16, 5, 1, 7, 3, CV, NT><<<blocks, NT, 0, s>>>(
         cview<_Float16>(&d0->x), dview<_Float16>(d0->y), dview<_Float16>(d1->y), d0->w, d0->bias, d1->w, d1->bias,
         d0->pad, d1->pad, d0->act, d1->act);
   else
-    dw_pair_kernel<float, 5, 1, 7, 3, CV><<<blocks, 256, 0, s>>>(
+    dw_pair_kernel<float, 5, 1, 7, 3, CV, NT><<<blocks, NT, 0, s>>>(
         cview<float>(&d0->x), dview<float>(d0->y), dview<float>(d1->y), d0->w, d0->bias, d1->w, d1->bias, d0->pad,
         d1->pad, d0->act, d1->act);
   return check_launch("ydbl_dwconv2d_pair_nhwc");
