@@ -15,6 +15,8 @@
 
 #include "common.hpp"
 
+extern "C" __device__ unsigned long long __ockl_wfred_or_u64(unsigned long long);  // DPP wave OR (ockl)
+
 #pragma clang fp contract(off)
 
 namespace ydbl {
@@ -508,17 +510,22 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
         const int wsrc = myc >> 6;
         const uint32_t rlo = __shfl((uint32_t)rem, wsrc), rhi = __shfl((uint32_t)(rem >> 32), wsrc);
         const uint64_t rw = ((uint64_t)rhi << 32) | rlo;
-        uint64_t M = __ballot(valid && !((rw >> (myc & 63)) & 1)), K = 0;
+        const uint64_t M = __ballot(valid && !((rw >> (myc & 63)) & 1));
         const int nk0 = nk;
-        // greedy inside the block on scalar registers: keep the first live rank, drop what it suppresses
-        while (M && nk < p.max_det) {
-          const int t = __ffsll((long long)M) - 1;
-          const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)dw, t);
-          const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(dw >> 32), t);
-          K |= 1ull << t;
-          M &= ~((((uint64_t)hi << 32) | lo) | (1ull << t));
-          ++nk;
+        // greedy inside the block: K_r = M_r & !(any s < r in K with D[s] bit r).  Iterated from K = M as
+        // K' = M & ~OR_{s in K} D[s] (one wave-wide OR per step) it reaches that unique fixed point: after t
+        // steps the first t ranks are final, and steps stop as soon as K repeats -- a few for NMS clusters,
+        // where the scalar walk paid one dependent step per kept rank
+        uint64_t K = M;
+        for (;;) {
+          const uint64_t W = __ockl_wfred_or_u64((K >> lane) & 1 ? dw : 0ull);
+          const uint64_t Kn = M & ~W;
+          if (Kn == K) break;
+          K = Kn;
         }
+        // keep[:max_det]: the greedy stops at max_det keeps, i.e. the lowest ranks of K
+        for (int extra = __popcll(K) - (p.max_det - nk0); extra > 0; --extra) K &= ~(1ull << (63 - __clzll(K)));
+        nk = nk0 + __popcll(K);
         if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = myc;
         // the kept candidates' rows join the removed flags (8 row reads in flight at a time)
         // (branch-free: all 8 reads are issued before the first OR)
