@@ -273,3 +273,36 @@ def test_map50_config5_dbl_s_640(golden_dir, mode):
         assert m_gpu > 0.3
     else:
         assert m_cpu - m_gpu <= 0.1
+
+
+@pytest.mark.parametrize("groups", ["1", "0"])
+def test_nms_paths_agree_on_model_candidates(golden_dir, monkeypatch, groups):
+    """The pair-matrix NMS path (images with <= 1024 candidates) against sort + chunked sweep on the
+    candidates the DBL-n model itself decodes at the bench protocol (640, conf .25, iou .7): identical
+    det / count, with the class split on and off."""
+    from ydbl import _lib
+    from ydbl._lib import NmsDesc
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    B = 32  # the bench batch: its busiest image has 644 candidates (11 rank blocks, 267 kept)
+    sess = p.session(B, 640, 640, half=True, conf=0.25, iou=0.7, max_det=300)
+    sess(blob_images(B, 640, seed=1234).cuda())
+    torch.cuda.synchronize()
+    assert int(sess.cand_count.max()) > 300  # clusters large enough for several rank blocks
+    cap = sess.cand_score.shape[1]
+    ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device="cuda")
+    outs = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("YDBL_NMS_FAST", fast)
+        monkeypatch.setenv("YDBL_NMS_GROUPS", groups)
+        out = torch.full((B, 300, 6), -1.0, device="cuda")
+        cnt = torch.full((B,), -1, dtype=torch.int32, device="cuda")
+        nd = NmsDesc(sess.cand_box.data_ptr(), sess.cand_score.data_ptr(), sess.cand_cls.data_ptr(),
+                     sess.cand_idx.data_ptr(), sess.cand_count.data_ptr(), B, cap, 0.7, 300, 30000, 0, 7680.0,
+                     640.0, 640.0, out.data_ptr(), cnt.data_ptr(), ws.data_ptr())
+        _lib.check(_lib.lib.ydbl_nms(nd, torch.cuda.current_stream().cuda_stream))
+        torch.cuda.synchronize()
+        outs.append((out, cnt))
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], sess.count) and torch.equal(outs[0][0], sess.det)
