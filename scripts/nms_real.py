@@ -4,6 +4,8 @@ the one-workgroup-per-image forms, and (with the stamps build, scripts/build_nms
 pointing at it) the slowest workgroup's phase split.
 
     python scripts/nms_real.py [--stamps]
+
+(build_dbg/ is listed in .gpurunignore; drop that line for a --stamps run on the GPU box.)
 """
 import argparse
 import ctypes as C

@@ -547,6 +547,12 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
     if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
     return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
   }
+  const char* b64 = getenv("YDBL_IGEMM_BN64");  // A/B knob (read per launch): 64-wide column blocks for Cout > 64
+  if (b64 && *b64 == '1') {
+    if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
+    if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
+    return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
+  }
   if (blocks(128, 128) >= want) return launch_igemm<T, Q8, 128, 128, 2, 2>(a, pointwise, s);
   if (blocks(64, 128) >= want) return launch_igemm<T, Q8, 64, 128, 2, 2>(a, pointwise, s);
   return launch_igemm<T, Q8, 32, 128, 2, 2>(a, pointwise, s);
