@@ -520,7 +520,7 @@ static void launch_igemm(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
 
 template <typename T, bool Q8>
 static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
-  // BN covers Cout in one column of workgroups where it can (the input tile is then read once);
+  // BN covers Cout <= 64 in one column of workgroups (the input tile is then read once; wider Cout: below);
   // BM is the largest pixel tile that still gives >= `want` workgroups: 512 (2 per CU) for small
   // maps whose Cout fits one 128-wide column (bigger pixel tiles re-read the weights less:
   // 512->128 1x1 @40^2 bs32 31.3 -> 23.0 us, 384->128 25.6 -> 19.4 us), 1024 otherwise
@@ -547,8 +547,12 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
     if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
     return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
   }
-  const char* b64 = getenv("YDBL_IGEMM_BN64");  // A/B knob (read per launch): 64-wide column blocks for Cout > 64
-  if (b64 && *b64 == '1') {
+  // Cout > 64: 64-wide column blocks (each workgroup stages half the weight rows; the input tile is read
+  // once per column block, from L2/MALL at these map sizes).  Measured against 128-wide blocks on the
+  // bench workloads: DBL-n bs32 14.82 -> 14.91 k img/s (bs16 graphs: 64->128 @80^2 22.6 -> 19.8 us,
+  // 128->192 @40^2 15.6 -> 12.1 us), DBL-s bs64 7.52 -> 7.57 k, DBL-l 1280 bs8 467 -> 466 (noise).
+  const char* b64 = getenv("YDBL_IGEMM_BN64");  // A/B knob (read per launch): 0 = 128-wide column blocks
+  if (!(b64 && *b64 == '0')) {
     if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
     if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
     return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
