@@ -300,16 +300,17 @@ __device__ unsigned long long g_nms_stamps[16 * 4096];
 
 // ---- pair-matrix path for images with n <= NMS_FAST candidates (the common case) --------------------
 // The greedy sweep of one image is serial, but everything it consumes is not: nms_pair_kernel spreads the
-// image's n x n candidate pairs over PW workgroups per image (one 64 x 64 block per wave) and writes, in
-// candidate (slot) order,
+// n x n candidate pairs of every image over the chip (64 x 64 blocks, one per workgroup at a time, each
+// wave testing 16 of the block's columns) and writes, in candidate (slot) order,
 //   fmask[b][i][w] bit s = IoU(box i, box 64w+s) > thr   (torchvision's decision, iou_gt; the IoU is
 //                                                         symmetric bit for bit, so row i is what box i
 //                                                         suppresses whichever of the two ranks first)
 //   frank[b][w][i]       = #{j in block w : key_j < key_i} (partial ranks; keys are unique)
 // and nms_kernel then only sums the ranks (rank = sort position, as the stable sort), stages the rows in
-// LDS and runs the sweep in rank order on one wave: a candidate is kept iff its bit in the running
-// removed mask is clear, and a kept candidate ORs its row into the mask.  Rows of candidates ranked
-// earlier get bits set too, which changes nothing: their decision is already made.
+// LDS and runs the sweep in rank order on one wave, 64 ranks at a time: a candidate is kept iff its bit
+// in the running removed mask is clear and no kept candidate earlier in its block suppresses it, and a
+// kept candidate ORs its row into the mask.  Rows of candidates ranked earlier get bits set too, which
+// changes nothing: their decision is already made.
 constexpr int NMS_FAST = 1024;        // candidates per image on this path (mask rows staged in LDS: 128 KiB)
 constexpr int NMS_FW = NMS_FAST / 64;  // 64-bit words per mask row
 
@@ -325,9 +326,9 @@ __device__ __forceinline__ float rlane(float v, int l) {
 constexpr int NMS_PAIR_MAXB = 1024;  // images per launch on the pair-matrix path (block offsets in LDS)
 constexpr int NMS_PAIR_WGS = 512;    // workgroups, each taking 64 x 64 blocks in turn
 
-// Persistent over all images' blocks: workgroups that would find an image with few candidates have no
-// idle launch cost (a (32 x images) grid spent ~20 us dispatching mostly empty workgroups), and the
-// blocks of a heavy image spread over the whole chip.
+// Persistent over all images' blocks: no workgroup is launched for an image with few candidates (a
+// (32 x images) grid of one block per wave took 22 us, mostly dispatching empty workgroups and walking a
+// block's 64 columns on one wave), and the blocks of a heavy image spread over the whole chip.
 __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
   __shared__ int s_pre[NMS_PAIR_MAXB + 1];  // s_pre[b] = blocks of images < b
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
