@@ -101,15 +101,61 @@ def dysample_traffic(step, elsize):
     return byts, 0.0
 
 
+def _v(v):
+    """(pixels, channels) of a ydbl_view struct or pointer to one (None / NULL view -> (0, 0))."""
+    if v is None:
+        return 0, 0
+    v = getattr(v, "contents", v)
+    return (_px(v), v.c) if v.ptr else (0, 0)
+
+
+def views_traffic(reads, writes, elsize, flops=0.0):
+    return (sum(p * c for p, c in map(_v, reads)) + sum(p * c for p, c in map(_v, writes))) * elsize, flops
+
+
+def other_traffic(step, elsize):
+    """Algorithmic bytes / FLOPs of the remaining launch kinds (activations read once and written
+    once at the run dtype; small weights and the NMS candidate lists are left out)."""
+    k, a = step.fn.__name__, step.args
+    if k == "ydbl_dwconv2d_pair_nhwc":
+        d0, d1 = a[0], a[1]
+        return views_traffic([d0.x], [d0.y, d1.y], elsize, 2.0 * _px(d0.y) * d0.y.c * (d0.kh * d0.kw + d1.kh * d1.kw))
+    if k == "ydbl_dwconv2d_nhwc":
+        d = a[0]
+        return views_traffic([d.x] + ([d.r] if d.res_mode else []), [d.y], elsize, 2.0 * _px(d.y) * d.y.c * d.kh * d.kw)
+    if k == "ydbl_lsk_gate":
+        return views_traffic([a[0]], [a[3]], elsize, 2.0 * _v(a[3])[0] * (98 * 2 + a[3].c * 2))
+    if k == "ydbl_pool_up_concat":
+        return views_traffic([a[0], a[1], a[2]], [a[3]], elsize)
+    if k == "ydbl_gate_add":
+        return views_traffic([a[0], a[1]], [a[3]], elsize)
+    if k in ("ydbl_hg_context", "ydbl_hg_propagate"):
+        d = a[0]
+        n, dd, e = _px(d.x), d.x.c, d.num_edges
+        if k == "ydbl_hg_context":
+            return views_traffic([d.x], [], elsize, 2.0 * d.x.n * e * dd * 2 * dd)
+        return views_traffic([d.x, d.xp], [d.y], elsize, 2.0 * n * (2 * e * dd + 2 * dd * dd))
+    if k == "ydbl_conv_stem":
+        n, cin, h, w, y = a[1], a[2], a[3], a[4], a[11]
+        return n * cin * h * w * 4 + _v(y)[0] * y.c * elsize, 2.0 * _v(y)[0] * y.c * 27
+    if k == "ydbl_detect_decode":
+        d = a[0]
+        reads = [d.box[i] for i in range(d.nl)] + [d.cls[i] for i in range(d.nl)]
+        return views_traffic(reads, [], elsize)
+    return 0.0, 0.0
+
+
 TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("dsconv", dsconv_traffic),
            "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
            "ydbl_dsbottleneck_nhwc": ("dsbottleneck", dsbneck_traffic),
            "ydbl_dysample_ex": ("dysample", dysample_traffic)}
 
 
-def roofline(session, dtype_name, reps=3, key=None):
+def roofline(session, dtype_name, reps=3, key=None, step_ms=None):
     """Per-launch HIP-event timing of one eager walk of every plan of the session (min of `reps`); the
-    dominant kernel family (most time) = the dense conv; a per-family table beside it."""
+    dominant kernel family (most time) = the dense conv; a per-family table beside it; and the
+    whole-network figure of SURVEY §8d: t_k = max(bytes_k / HBM peak, flops_k / MFMA peak) per launch,
+    sum over every launch of the step, divided by the measured step time `step_ms` of the timed run."""
     elsize = 4 if dtype_name == "fp32" else 2  # activation bytes (fp8 mode keeps fp16 activations)
     steps, best = [], []
     for plan in session.plans:  # one plan per sub-batch stream (each launch timed on its own)
@@ -132,6 +178,20 @@ def roofline(session, dtype_name, reps=3, key=None):
             e["bytes"] += b
             e["flops"] += f
     pk = MFMA_PEAK_TFLOPS[dtype_name]
+    net_b = net_f = t_roof = 0.0
+    for st in steps:
+        kind = st.fn.__name__
+        b, f = TRAFFIC[kind][1](st, elsize) if kind in TRAFFIC else other_traffic(st, elsize)
+        net_b, net_f = net_b + b, net_f + f
+        t_roof += max(b / (HBM_PEAK_GBS * 1e9), f / (pk * 1e12))
+    eager_ms = sum(ms for _, ms in best)
+    network = {"launches_per_step": len(steps), "alg_bytes_per_step": int(net_b), "alg_flops_per_step": net_f,
+               "roofline_ms_per_step": round(t_roof * 1e3, 4), "eager_ms_per_step": round(eager_ms, 4),
+               "frac_of_eager": round(t_roof * 1e3 / eager_ms, 4),
+               "rule": "sum_k max(bytes_k / 8 TB/s, flops_k / MFMA peak) over every launch of the step "
+                       "(algorithmic bytes: activations read + written once, weights once) / step time"}
+    if step_ms:
+        network.update({"measured_ms_per_step": round(step_ms, 4), "frac": round(t_roof * 1e3 / step_ms, 4)})
     pmc = pmc_summary(key)
     families = {}
     for name, e in sorted(fam.items(), key=lambda kv: -kv[1]["ms"]):
@@ -160,7 +220,7 @@ def roofline(session, dtype_name, reps=3, key=None):
                "avg_launch_us": round(c["ms"] * 1e3 / c["launches"], 2),
                "alg_bytes_per_launch": int(c["bytes"] / c["launches"]), "alg_flops_per_step": c["flops"],
                "arith_intensity": round(ai, 1), "tflops": round(ach_tf, 2),
-               "eager_step_ms": round(sum(ms for _, ms in best), 3),
+               "eager_step_ms": round(eager_ms, 3), "network": network,
                "ms_by_kernel": {k: round(v, 3) for k, v in sorted(by_kind.items(), key=lambda kv: -kv[1])},
                "traffic": pc.get("hbm_bytes_per_launch"), "mfma_busy": pc.get("mfma_busy"),
                "code_hash": code_hash(),
@@ -246,7 +306,11 @@ def cpu_baseline(model_key, imgsz, batch, budget_s=10.0, gpu_session=None):
 
     legs = [leg(batch, threads_all), leg(1, 1)]
     torch.set_num_threads(threads_all)
-    out = {"value": legs[0]["img_per_s"], "unit": "images/s", "cores": threads_all, "kind": "port",
+    # `cores` = the threads actually used (torch intra-op threads of this process on the box's CPU share);
+    # os_cpu_count is the whole machine's logical CPUs, most of which belong to other jobs
+    out = {"value": legs[0]["img_per_s"], "unit": "images/s", "cores": threads_all, "threads": threads_all,
+           "cores_note": f"{threads_all} intra-op threads (= cores used) of {os.cpu_count()} logical CPUs on the host",
+           "kind": "port",
            "sample": f"{legs[0]['iters']} x bs{batch} DBL-{model_key} {imgsz}x{imgsz} nc3 fp32 oracle forward+NMS "
                      f"on {threads_all} threads ({legs[0]['secs']} s); 1-thread leg: {legs[1]['img_per_s']} img/s",
            "legs": legs, "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count()}
@@ -281,11 +345,12 @@ def accuracy_check(m, gpu, imgsz, n=8):
     dm.process(*(torch.cat(st[k]).numpy() for k in ("tp", "conf", "pred_cls", "target_cls")))
     batch = {"img": x, "cls": torch.cat([lb[:, 0] for lb in labels]), "bboxes": torch.cat([lb[:, 1:] for lb in labels]),
              "batch_idx": torch.cat([torch.full((len(lb),), i) for i, lb in enumerate(labels)])}
-    yolo, fp8 = gpu  # the product YOLO (HIP path) and whether the bench runs e4m3 operands
-    m_gpu = yolo.val(data=[batch], half=True, fp8=fp8).box.map50
+    yolo, fp8, half = gpu  # the product YOLO (HIP path), e4m3 operands or not, fp16 or fp32 (the timed path)
+    m_gpu = yolo.val(data=[batch], half=half, fp8=fp8).box.map50
     return {"gpu": round(float(m_gpu), 4), "cpu": round(float(dm.box.map50), 4),
             "drop": round(float(dm.box.map50 - m_gpu), 4),
             "images": n, "gt_boxes": int(sum(len(lb) for lb in labels)),
+            "gpu_precision": "fp8" if fp8 else ("fp16" if half else "fp32"),
             "protocol": "pseudo-GT = CPU oracle detections at conf .25; val NMS conf .001 multi-label iou .7"}
 
 
@@ -394,6 +459,8 @@ def main():
     extra = {"dets_per_image": round(float(sess.count.float().mean().item()), 2),
              "candidates_per_image": round(float(sess.cand_count.float().mean().item()), 1),
              "candidates_max": int(sess.cand_count.max().item())}
+    if args.fp8:  # achieved share of the candidate MACs in e4m3 (output-pixel MACs, ydbl.quant.candidate_macs)
+        extra["fp8_mac_fraction"] = round(float(sess.fp8_mac_fraction), 4)
     rf = None
     if rank == 0 and not args.no_roofline:
         # The roofline describes the kernels at the headline launch size: one launch per layer over the
@@ -407,11 +474,11 @@ def main():
             rsess.load(blob_images(B, S, seed=1234 + rank).to(dev))
             rsess()
             rkey = key.replace(f"streams={args.streams}", "streams=1")
-        rf = roofline(rsess, dtype_name, key=rkey)
+        rf = roofline(rsess, dtype_name, key=rkey, step_ms=el * 1e3 / args.steps)
         rf["plan"] = f"full-batch plan (bs {B}, one launch per layer); timed run on {args.streams} stream(s)"
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.model, S, B, gpu_session=(model, fp8))
+        cpu = cpu_baseline(args.model, S, B, gpu_session=(model, fp8, half))
     if rank == 0:
         emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu)
     if world > 1:
@@ -460,7 +527,7 @@ def emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu):
                                f"(conf .25, iou .7, max_det 300)" + (", RCCL all-gather of boxes" if world > 1 else ""),
                    "model": Path(cfg).stem, "global_batch": B * world, "imgsz": S, "nc": 3,
                    "parallelism": f"dp{world}", "streams_per_gpu": args.streams,
-                   **({"fp8_mac_fraction": min(args.fp8, 1.0)} if args.fp8 else {})},
+                   **({"fp8_mac_fraction": extra.pop("fp8_mac_fraction", None)} if args.fp8 else {})},
         **extra,
         "roofline": rf,
         "cpu_baseline": cpu,

@@ -177,7 +177,8 @@ int ydbl_gate_add(const ydbl_view* a, const ydbl_view* b, float gate, const ydbl
 int ydbl_pool_up_concat(const ydbl_view* p_lo, const ydbl_view* p_mid, const ydbl_view* p_hi,
                         const ydbl_view* y, void* stream);
 
-/* DySample 'lp' x2 sampling: off fp32 view [n,h,w,8*groups] holding 0.25*offset+init_pos
+/* DySample 'lp' x2 sampling: off view [n,h,w,8*groups] in x's dtype (fp16 in half mode, as the reference's
+ * .half() offset conv produces it) holding 0.25*offset+init_pos
  * (channel k = coord*4g + group*4 + i*2 + j), bilinear border grid_sample of x into y [n,2h,2w,c]. */
 int ydbl_dysample(const ydbl_view* x, const ydbl_view* off, int32_t groups, const ydbl_view* y, void* stream);
 /* Same, descriptor form with an optional second output (y2.ptr != NULL): y2 = a2 * y + b2 * r2 -- a

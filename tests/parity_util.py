@@ -195,3 +195,73 @@ def gpu_pred(p, x, half=False, fp8=False, conf=0.25, iou=0.7, calib=None, stream
     s(x.cuda())
     torch.cuda.synchronize()
     return s.pred.cpu(), s.results()
+
+
+@torch.inference_mode()
+def fp8_emulated_leg(o, x, plan):
+    """What fp8 (BASELINE config 5) does to the reference path on its own: the oracle's fp16 leg (the reference's
+    half=True path, evaluated by torch-CPU) with every convolution / linear layer that the GPU `plan` switched to
+    e4m3 operands (ydbl.quant.enable_fp8: plan.fp8_switched) replaced by its e4m3 emulation at the GPU's
+    calibrated scales: input x -> e4m3(x * qs) / qs, weights per output row -> e4m3(w * sw) / sw with
+    sw = 448 / max|w_row|, then the fp32 conv + bias.  The plan's candidates are matched to the oracle's modules
+    by their (scale-normalised) weight rows, so merged launches (C3's cv2 + cv1) and folded constants
+    (DySample's 0.25) map back to the reference's own layers.  Returns (decoded predictions [B, 4+nc, A] fp32,
+    number of oracle layers emulated)."""
+    import types
+
+    import torch.nn as nn
+    import torch.nn.functional as F
+
+    from ydbl.quant import E4M3_MAX, e4m3_round
+
+    rows, owner = [], []  # normalised leading 16 values of every switched candidate row, and (qs, cin_pad)
+    for ci in plan.fp8_switched:
+        d, xv, w32 = plan.fp8_candidates[ci]
+        w = w32[:, : d.kh * d.kw * xv.c].double()
+        w = w / w.abs().amax(1, keepdim=True).clamp_min(1e-30)
+        rows.append(w[:, :16])
+        owner += [(float(d.qscale), xv.c)] * w.shape[0]
+    if not rows:
+        raise ValueError("the plan has no fp8-switched convolutions")
+    rows = torch.cat(rows)
+    m = copy.deepcopy(o).half()
+    n_emulated = 0
+    for ref_mod, mod in zip(o.modules(), m.modules()):
+        if isinstance(ref_mod, nn.Conv2d) and ref_mod.groups == 1:
+            w = ref_mod.weight.detach().double()
+            co, ci, kh, kw = w.shape
+        elif isinstance(ref_mod, nn.Linear):
+            w = ref_mod.weight.detach().double()[:, :, None, None]
+            co, ci, kh, kw = w.shape
+        else:
+            continue
+        sig = w[0].permute(1, 2, 0)  # [kh][kw][ci] tap-major, as the plan's weight matrix
+        hit = None
+        for cin_pad in {c for _, c in owner}:
+            if cin_pad < ci:
+                continue
+            r = F.pad(sig, (0, cin_pad - ci)).reshape(-1)
+            r = (r / r.abs().max().clamp_min(1e-30))[:16]
+            dev = (rows[:, : len(r)] - r).abs().amax(1)
+            j = int(dev.argmin())
+            if dev[j] < 1e-5 and owner[j][1] == cin_pad:
+                hit = owner[j]
+                break
+        if hit is None:
+            continue
+        qs = hit[0]
+        w32 = ref_mod.weight.detach().float()
+        sw = E4M3_MAX / w32.reshape(co, -1).abs().amax(1).clamp_min(1e-12)
+        shape = (-1,) + (1,) * (w32.dim() - 1)
+        wq = e4m3_round(w32 * sw.view(shape)) / sw.view(shape)
+        b32 = ref_mod.bias.detach().float() if ref_mod.bias is not None else None
+
+        def fwd(self, inp, wq=wq, b32=b32, qs=qs, conv=isinstance(ref_mod, nn.Conv2d)):
+            xq = e4m3_round(inp.float() * qs) / qs
+            y = (F.conv2d(xq, wq, b32, self.stride, self.padding, self.dilation) if conv else F.linear(xq, wq, b32))
+            return y.to(inp.dtype)
+
+        mod.forward = types.MethodType(fwd, mod)
+        n_emulated += 1
+    y, _ = m(x.half())
+    return y.float(), n_emulated

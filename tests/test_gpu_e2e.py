@@ -23,8 +23,8 @@ compared with y64:
 import pytest
 import torch
 
-from parity_util import (class_agreement, detections, err_stats, fp16_rule, fp32_rule, gpu_pred, load_e2e,
-                         match_detections, ROLE_FX)
+from parity_util import (build_pair, class_agreement, detections, err_stats, fp16_rule, fp32_rule, fp8_emulated_leg,
+                         gpu_pred, load_e2e, match_detections, ROLE_FX)
 
 pytestmark = pytest.mark.gpu
 
@@ -105,3 +105,45 @@ def test_e2e_fp16(golden_dir, name, batch, streams):
     print(f"   detections: {m['pairs']} pairs, {m['borderline']} borderline, {len(m['mismatches'])} mismatches "
           f"(ref half path: {o16['det_mismatches']})")
     assert len(m["mismatches"]) <= 2 * o16["det_mismatches"] + 2, m["mismatches"][:5]
+
+
+@pytest.mark.parametrize("fraction", [0.25, 1.0])
+def test_e2e_fp8_config5(golden_dir, fraction):
+    """BASELINE config 5 end to end at its own batch and the bench layout: DBL-s 640, bs 32, two sub-batch
+    streams, e4m3 operands on `fraction` of the candidate MACs (0.25 = the bench's config-5 setting, 1.0 = all),
+    one joint calibration on a separate batch (bench.py).  The reference has no fp8 path, so the bound is
+    derived the fp16 rule's way from the fp8 leg of the reference computation itself: the oracle's fp16 leg
+    with the very layers the GPU switched emulated in e4m3 at the GPU's scales (parity_util.fp8_emulated_leg).
+    GPU box / score deviation from fp64 (max, p99.9) <= 2x that leg's + the fp16 rule's floors; final
+    detections matched both ways with <= 2x that leg's mismatches + 2."""
+    from ydbl.utils.synthetic import blob_images
+
+    y64, meta = load_e2e(golden_dir, "s640")
+    S, ref, conf, iou = meta["imgsz"], meta["ref_images"], meta["conf"], meta["iou"]
+    x = blob_images(meta["batch_full"], S, seed=meta["seed"])
+    assert x.shape[0] == 32
+    p, o = build_pair("s", 3, golden_dir)
+    s = p.session(32, S, S, half=True, conf=conf, iou=iou, keep_pred=True, fp8=True if fraction >= 1 else fraction,
+                  streams=2)
+    s.calibrate_fp8(blob_images(32, S, seed=4321).cuda())
+    s(x.cuda())
+    torch.cuda.synchronize()
+    yg = s.pred.cpu()[ref]
+    dets = [s.results()[i] for i in ref]
+    assert [c.plan.fp8_switched for c in s.children][0] == s.children[1].plan.fp8_switched  # one joint selection
+    ye, n_emul = fp8_emulated_leg(o, x[ref], s.children[0].plan)
+    assert n_emul >= len(s.children[0].plan.fp8_switched)
+    ref_dets = detections(y64, conf, iou, (S, S))
+    st_e, st_g = err_stats(ye, y64), err_stats(yg, y64)
+    tb, tc = fp16_rule(st_e)
+    m_e = match_detections(ref_dets, detections(ye, conf, iou, (S, S)), y64, conf, iou, tb, tc)
+    m_g = match_detections(ref_dets, dets, y64, conf, iou, tb, tc)
+    print(f"s640 bs32 fp8 (MAC fraction {s.fp8_mac_fraction:.3f}, {len(s.children[0].plan.fp8_switched)} convs, "
+          f"{n_emul} oracle layers emulated): gpu box max/p99.9 {st_g['box_max']:.3g}/{st_g['box_p999']:.3g} px "
+          f"(emulated ref {st_e['box_max']:.3g}/{st_e['box_p999']:.3g}), score max/p99.9 "
+          f"{st_g['conf_max']:.3g}/{st_g['conf_p999']:.3g} (ref {st_e['conf_max']:.3g}/{st_e['conf_p999']:.3g}); "
+          f"detections {m_g['pairs']} pairs, {len(m_g['mismatches'])} mismatches (emulated ref "
+          f"{len(m_e['mismatches'])})")
+    for k in ("box_max", "box_p999", "conf_max", "conf_p999"):
+        assert st_g[k] <= 2 * st_e[k] + (1e-2 if k.startswith("box") else 1e-4), (k, st_g, st_e)
+    assert len(m_g["mismatches"]) <= 2 * len(m_e["mismatches"]) + 2, m_g["mismatches"][:5]

@@ -91,9 +91,10 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
     (192, 3, 1, 7, 9, None, False),        # Cout 3 (Detect cls width), K 192
     (32, 16, 4, 33, 5, "add", False),      # K 32, one k-step
 ])
-def test_conv1x1_one_shot(cin, cout, n, h, w, res, second):
-    """fp16 pointwise convs with K <= 256 take conv1x1.hip (all loads of a workgroup in one round
-    trip): vs F.conv2d fp32 on the fp16-rounded operands, input/output as channel slices."""
+def test_conv1x1_shapes(cin, cout, n, h, w, res, second):
+    """fp16 pointwise convs at the DBL neck's shapes (conv.hip conv_igemm_kernel, block-tiled implicit GEMM):
+    vs F.conv2d fp32 on the fp16-rounded operands, input/output as channel slices, residual add / multiply
+    and the fused FullPAD second output."""
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense
 

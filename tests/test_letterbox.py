@@ -114,3 +114,85 @@ def test_predict_frames_matches_tensor_path():
         scale_boxes(xb.shape[2:], ref, frames[i].shape[:2])
         assert torch.equal(res[i].boxes.data, ref)
         assert res[i].orig_shape == frames[i].shape[:2]
+
+
+def _write_pngs(tmp_path, frames, names):
+    from PIL import Image
+
+    paths = []
+    for f, n in zip(frames, names):
+        p = tmp_path / n
+        Image.fromarray(np.ascontiguousarray(f[:, :, ::-1])).save(p)  # BGR frame -> RGB file
+        paths.append(p)
+    return paths
+
+
+def test_sources_file_collection(tmp_path):
+    """LoadImagesAndVideos file rules (U/data/loaders.py:328-351): dir = sorted *.*, glob, *.txt relative to its
+    folder, images only; PIL / ndarray sources decode to the BGR frames cv2 would give (lossless PNG)."""
+    from PIL import Image
+
+    from ydbl.engine.sources import frames_from_images, image_files
+
+    frames = _frames([(40, 60), (30, 20), (50, 50)], seed=5)
+    paths = _write_pngs(tmp_path, frames, ["b.png", "a.png", "c.png"])
+    (tmp_path / "notes.json").write_text("{}")
+    want = [str(tmp_path / n) for n in ("a.png", "b.png", "c.png")]
+    assert image_files(tmp_path) == want
+    assert image_files(str(tmp_path / "*.png")) == want
+    (tmp_path / "list.txt").write_text("c.png\nb.png\n")
+    assert image_files(tmp_path / "list.txt") == [want[1], want[2]]  # list entries sorted, as the reference
+    with pytest.raises(FileNotFoundError):
+        image_files(tmp_path / "missing.png")
+    ps, got = frames_from_images([Image.open(paths[0]), str(paths[1]), frames[2]])
+    assert ps == [str(paths[0]), str(paths[1]), "image2.jpg"]
+    for g, f in zip(got, frames):
+        assert g.dtype == np.uint8 and np.array_equal(g, f)
+
+
+@pytest.mark.gpu
+def test_predict_file_dir_glob_pil_sources(tmp_path):
+    """predict() on a file, a directory, a glob, a *.txt list and PIL images gives the ndarray-frame path's
+    detections (same frames, same batch composition), with the file paths on the Results."""
+    from PIL import Image
+
+    from ydbl import YOLO
+    from ydbl.utils.synthetic import blob_images
+
+    m = YOLO("yolov13n_DBL.yaml", nc=3)
+    x = blob_images(2, 256, seed=11)
+    frames = [np.ascontiguousarray((x[i].permute(1, 2, 0).numpy()[:, :, ::-1] * 255).round().astype(np.uint8))
+              for i in range(2)]
+    paths = _write_pngs(tmp_path, frames, ["f0.png", "f1.png"])
+    one = [m.predict(f, imgsz=256, conf=0.05)[0] for f in frames]  # batch of one frame each
+    both = m.predict(frames, imgsz=256, conf=0.05)
+    assert sum(len(r.boxes.data) for r in both) > 0
+    cases = [(m.predict(str(paths[0]), imgsz=256, conf=0.05), one[:1]),
+             (m.predict(tmp_path, imgsz=256, conf=0.05), one),
+             (list(m.predict(str(tmp_path / "*.png"), imgsz=256, conf=0.05, stream=True)), one),
+             (m.predict(tmp_path, imgsz=256, conf=0.05, batch=2), both),
+             (m.predict([Image.open(p) for p in paths], imgsz=256, conf=0.05), both),
+             (m.predict([str(p) for p in paths], imgsz=256, conf=0.05), both)]
+    (tmp_path / "l.txt").write_text("f1.png\n")
+    cases.append((m.predict(tmp_path / "l.txt", imgsz=256, conf=0.05), one[1:]))
+    for got, want in cases:
+        assert len(got) == len(want)
+        for g, w in zip(got, want):
+            assert torch.equal(g.boxes.data, w.boxes.data)
+    assert m.predict(tmp_path, imgsz=256, conf=0.05)[1].path == str(paths[1])
+
+
+@pytest.mark.gpu
+def test_session_cache_is_bounded():
+    """Model._sessions is an LRU of MAX_SESSIONS entries: predict() over many batch sizes does not keep every
+    compiled session (and its HBM) alive."""
+    from ydbl import YOLO
+
+    m = YOLO("yolov13n_DBL.yaml", nc=3)
+    for b in range(1, m.MAX_SESSIONS + 3):
+        m.predict(torch.rand(b, 3, 64, 64), conf=0.5)
+    assert len(m._sessions) == m.MAX_SESSIONS
+    keys = list(m._sessions)
+    assert [k[0] for k in keys] == list(range(3, m.MAX_SESSIONS + 3))
+    m.predict(torch.rand(3, 3, 64, 64), conf=0.5)  # hit: becomes most recent
+    assert list(m._sessions)[-1][0] == 3

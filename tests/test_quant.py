@@ -1,0 +1,40 @@
+"""fp8 mixed-precision selection (ydbl.quant): MAC accounting and the MAC-budget pick, host logic only."""
+
+from types import SimpleNamespace as NS
+
+import torch
+
+from ydbl.quant import candidate_macs, select_by_mac_budget
+
+
+def _cand(cin, cout, k, s, h, w, n=2):
+    """(desc, input view, fp32 [Cout][KPAD] weights) as Plan.fp8_candidates holds them."""
+    ho, wo = (h + 2 * (k // 2) - k) // s + 1, (w + 2 * (k // 2) - k) // s + 1
+    kpad = (k * k * cin + 31) // 32 * 32
+    d = NS(kh=k, kw=k, y=NS(n=n, h=ho, w=wo, c=cout))
+    return d, NS(n=n, h=h, w=w, c=cin), torch.zeros(cout, kpad)
+
+
+def test_candidate_macs_use_output_pixels_and_real_k():
+    c1 = _cand(64, 64, 3, 2, 80, 80)  # the stride-2 downsample: 40x40 outputs
+    assert candidate_macs(c1) == 64 * 9 * 64 * 2 * 40 * 40
+    c2 = _cand(72, 16, 1, 1, 40, 40)  # K = 72 (KPAD 96 is padding, not MACs)
+    assert candidate_macs(c2) == 16 * 72 * 2 * 40 * 40
+
+
+def test_selected_fraction_with_a_stride2_candidate():
+    """One stride-2 candidate among stride-1 ones: the switched share of MACs is computed on output pixels, so
+    `fraction` of the real MACs is switched (input-pixel counting would have priced the s2 conv 4x)."""
+    cands = [_cand(64, 64, 3, 2, 80, 80), _cand(128, 128, 1, 1, 40, 40), _cand(64, 64, 1, 1, 40, 40)]
+    macs = [candidate_macs(c) for c in cands]  # 118.0M, 52.4M, 13.1M
+    total = sum(macs)
+    # least sensitive first: the s2 conv (64 % of the MACs) fits a 0.7 budget alone; counted on its input
+    # pixels (472M of 537M) it would not, and the two 1x1s would be switched instead
+    chosen, frac = select_by_mac_budget([0.1, 0.9, 0.2], macs, 0.7)
+    assert chosen == [0] and abs(frac - macs[0] / total) < 1e-12 and frac <= 0.7
+    chosen, frac = select_by_mac_budget([0.1, 0.9, 0.2], macs, 0.5)  # s2 too big: skipped, the rest fit
+    assert chosen == [1, 2] and frac <= 0.5
+    chosen, frac = select_by_mac_budget([0.1, 0.9, 0.2], macs, 1.0)
+    assert chosen == [0, 1, 2] and frac == 1.0
+    chosen, frac = select_by_mac_budget([0.1, 0.9, 0.2], macs, 0.0)
+    assert chosen == [] and frac == 0.0

@@ -232,7 +232,7 @@ __device__ __forceinline__ void dw_pair_phase(const typename Vec<T>::type* src, 
     if (keep) {
       vec t;
 #pragma unroll
-      for (int q = 0; q < V; ++q) t[q] = (T)o[q];
+      for (int q = 0; q < V; ++q) t[q] = (T)round_to<T>(o[q]);  // the same pinned rounding as the stored y0
       keep[p * CV + cv] = t;
     }
   }

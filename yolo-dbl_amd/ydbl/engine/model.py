@@ -12,7 +12,9 @@ execution path (``device='cpu'`` raises).
 
 from __future__ import annotations
 
+import os
 import time
+from collections import OrderedDict
 from pathlib import Path
 
 import numpy as np
@@ -72,7 +74,7 @@ class Model:
         self.overrides = {}
         self.ckpt_path = None
         self.verbose = verbose
-        self._sessions = {}
+        self._sessions = OrderedDict()  # LRU of compiled sessions (each holds its own HBM buffers)
         model = str(model)
         suffix = Path(model).suffix.lower()
         if suffix in (".pt", ".pth"):
@@ -148,6 +150,8 @@ class Model:
         return {"layers": len(self.model.model), "parameters": n}
 
     # ------------------------------------------------------------------ inference
+    MAX_SESSIONS = 4  # a DBL-n bs32 640 fp16 session holds ~0.95 GB of HBM: keep the few most recently used
+
     def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
                 multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True,
                 streams=1) -> DetectSession:
@@ -157,28 +161,51 @@ class Model:
         dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
-               float(fp8), bool(clip), int(streams))
+               float(fp8), bool(clip), int(streams),
+               # the kernels' A/B routing knobs are read at launch time, so a captured graph keeps the routing
+               # of its capture: a different knob setting is a different session
+               tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("YDBL_"))))
         s = self._sessions.get(key)
         if s is None:
+            while len(self._sessions) >= self.MAX_SESSIONS:
+                self._sessions.popitem(last=False)  # least recently used; its buffers go with the last reference
             with torch.cuda.device(dev):
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
                                   keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip,
                                   streams=streams)
             self._sessions[key] = s
+        else:
+            self._sessions.move_to_end(key)
         return s
 
     def predict(self, source=None, stream=False, **kwargs):
         """U/engine/model.py:501-560 + DetectionPredictor.postprocess (U/models/yolo/detect/predict.py:23-41).
 
-        source: BCHW float tensor (LoadTensor rules), or HWC uint8 BGR ndarray frame(s), which are
-        letterboxed to imgsz on the GPU and whose boxes come back in frame coordinates.
+        source (ydbl.engine.sources, after load_inference_source U/data/build.py:182-215):
+          - BCHW float tensor (LoadTensor rules): run as given;
+          - PIL image(s), HWC uint8 BGR ndarray frame(s), or a list of image paths (LoadPilAndNumpy): one batch;
+          - str / Path: an image file, a directory, a glob or a *.txt list (LoadImagesAndVideos): batches of
+            ``batch`` images (default 1) in sorted file order.
+        Non-tensor sources are letterboxed to imgsz on the GPU and their boxes come back in the original
+        image's coordinates.
         """
+        from .sources import check_path_source, file_batches, frames_from_images, is_frame_source
+
         args = {**DEFAULTS, **self.overrides, **kwargs}
         dev = select_device(args["device"])
         t0 = time.perf_counter()
-        if isinstance(source, np.ndarray) or (isinstance(source, (list, tuple)) and source
-                                               and isinstance(source[0], np.ndarray)):
-            return self._predict_frames(source, args, dev, t0, stream)
+        if source is None:
+            raise ValueError("predict() needs a source (no default asset is bundled)")
+        if not isinstance(source, torch.Tensor) and not (isinstance(source, (list, tuple)) and source
+                                                         and isinstance(source[0], torch.Tensor)):
+            if check_path_source(source):
+                gen = (r for paths, frames in file_batches(source, args["batch"])
+                       for r in self._predict_frames(frames, args, dev, time.perf_counter(), False, paths))
+                return gen if stream else list(gen)
+            if is_frame_source(source):
+                paths, frames = frames_from_images(source)
+                return self._predict_frames(frames, args, dev, t0, stream, paths)
+            raise TypeError(f"unsupported source type {type(source).__name__}")
         im = load_tensor_source(source, int(self.model.stride.max()))
         im = im.to(dev, non_blocking=True).float()
         b, _, h, w = im.shape
@@ -193,7 +220,7 @@ class Model:
                            boxes=det[i, : counts[i]].clone(), speed=speed) for i in range(b)]
         return iter(results) if stream else results
 
-    def _predict_frames(self, frames, args, dev, t0, stream):
+    def _predict_frames(self, frames, args, dev, t0, stream, paths=None):
         from .preprocess import letterbox_batch, scale_boxes
 
         frames = [frames] if isinstance(frames, np.ndarray) and frames.ndim == 3 else list(frames)
@@ -214,7 +241,8 @@ class Model:
         for i, f in enumerate(frames):
             boxes = det[i, : counts[i]].clone()
             scale_boxes((h, w), boxes, f.shape[:2])
-            results.append(Results(f, path=f"image{i}.jpg", names=self.model.names, boxes=boxes))
+            results.append(Results(f, path=paths[i] if paths else f"image{i}.jpg", names=self.model.names,
+                                   boxes=boxes))
         t3 = time.perf_counter()
         speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b,
                  "postprocess": (t3 - t2) * 1e3 / b}

@@ -142,14 +142,28 @@ class DetectSession:
         if x is not None:
             self.load(x)
         frac = self.fp8_fraction if fraction is None else float(fraction)
-        if self.children:
-            n = sum(c.calibrate_fp8(fraction=frac) for c in self.children)
-            self.fp8_ready = True
-            return n
-        n = enable_fp8(self.plan, self.plan.run, fraction=frac, head=self.compiled.feats)
-        self._graph = None  # descriptors changed: recapture
+        # one joint calibration over every sub-batch plan (ydbl.quant.enable_fp8): the same activation scales
+        # and the same fp8 layer set for every image of the batch, whichever stream it runs on
+        owners = self.children or [self]
+
+        def run_all():
+            for c in owners:
+                c.plan.run()
+
+        def heads():
+            return [t for c in owners for t in c.compiled.feats()]
+
+        n = enable_fp8([c.plan for c in owners], run_all, fraction=frac, head=heads)
+        for c in owners:
+            c._graph = None  # descriptors changed: recapture
+            c.fp8_ready = True
         self.fp8_ready = True
         return n
+
+    @property
+    def fp8_mac_fraction(self) -> float | None:
+        """Share of the fp8 candidates' MACs switched to e4m3 (None before calibration)."""
+        return getattr(self.plan, "fp8_mac_fraction", None)
 
     def launch(self):
         if self.fp8 and not self.fp8_ready:

@@ -41,27 +41,63 @@ def _switch(d, state):
         d.w, d.dq, d.qscale = state
 
 
-def enable_fp8(plan, run_calibration, select=None, fraction=1.0, head=None) -> int:
-    """Calibrate activation scales with one fp16 pass and switch fp8 candidate convs of `plan` to e4m3
-    operands.  `run_calibration()` must execute the plan once on calibration images.  fraction < 1 needs
-    `head()` (the Detect head outputs, list of tensors) and keeps the most sensitive convs in fp16.
-    Returns the number of convolutions switched."""
+def candidate_macs(cand) -> int:
+    """MACs of one fp8 candidate launch (desc, input view, fp32 [Cout][KPAD] weights): Cout x the real
+    K (kh * kw * Cin, not the padded KPAD) x OUTPUT pixels (a stride-2 conv has a quarter of its input's)."""
+    d, x, w = cand
+    return int(w.shape[0]) * int(d.kh * d.kw * x.c) * int(d.y.n * d.y.h * d.y.w)
+
+
+def select_by_mac_budget(sens, macs, fraction):
+    """Indices switched to e4m3 for a MAC `fraction`: least sensitive first, each taken while the running
+    MAC sum stays within fraction * total (a candidate that would overshoot is skipped, smaller ones after
+    it may still fit).  Returns (sorted indices, achieved MAC fraction)."""
+    order = sorted(range(len(sens)), key=lambda i: sens[i])
+    budget, used, chosen = fraction * sum(macs), 0, []
+    for i in order:
+        if used + macs[i] > budget + 1e-9:
+            continue
+        chosen.append(i)
+        used += macs[i]
+    return sorted(chosen), (used / sum(macs) if macs else 0.0)
+
+
+def enable_fp8(plans, run_calibration, select=None, fraction=1.0, head=None) -> int:
+    """Calibrate activation scales with one fp16 pass and switch fp8 candidate convs to e4m3 operands.
+
+    `plans`: one Plan, or the per-sub-batch plans of a split session (built from the same model, so their
+    candidate lists are parallel).  Calibration is joint: `run_calibration()` must execute EVERY plan once
+    on the calibration images, each candidate's activation scale is taken from the amax of its input over
+    all plans (the whole batch), the sensitivity ranking (fraction < 1) is done once on the whole batch
+    (`head()` returns the Detect head outputs of all plans), and the same scales and the same layer set go
+    to every plan, so an image gets the same fp8 layers whichever sub-batch it lands in.
+    Returns the number of convolutions switched per plan."""
+    plans = list(plans) if isinstance(plans, (list, tuple)) else [plans]
     run_calibration()
-    torch.cuda.synchronize(plan.device)
-    cands = [c for i, c in enumerate(plan.fp8_candidates) if select is None or select(i)]
-    if not cands:
+    for p in plans:
+        torch.cuda.synchronize(p.device)
+    idx = [i for i in range(len(plans[0].fp8_candidates)) if select is None or select(i)]
+    assert all(len(p.fp8_candidates) == len(plans[0].fp8_candidates) for p in plans), "plans differ"
+    if not idx:
         return 0
-    amaxes = torch.stack([x.torch().abs().amax().float() for _, x, _ in cands]).cpu()
-    states = []
-    for (d, _x, w32), ax in zip(cands, amaxes.tolist()):
+    amax = torch.stack([torch.stack([p.fp8_candidates[i][1].torch().abs().amax().float() for i in idx]).cpu()
+                        for p in plans]).amax(0)
+    states = [[] for _ in plans]  # per plan, per selected candidate: (w e4m3 ptr, dq ptr, qs)
+    for k, (i, ax) in enumerate(zip(idx, amax.tolist())):
         qs = E4M3_MAX / ax if ax > 0 else 1.0
-        wq, sw = quantize_weights_e4m3(w32)
-        wd = plan.const(wq.contiguous())
-        dq = plan.const((1.0 / (sw * qs)).float())
-        if not hasattr(d, "_w16"):
-            d._w16 = d.w
-        states.append((wd.data_ptr(), dq.data_ptr(), float(qs)))
-    order = list(range(len(cands)))
+        wq, sw = quantize_weights_e4m3(plans[0].fp8_candidates[i][2])
+        dqv = (1.0 / (sw * qs)).float()
+        for pi, p in enumerate(plans):
+            d = p.fp8_candidates[i][0]
+            if not hasattr(d, "_w16"):
+                d._w16 = d.w
+            states[pi].append((p.const(wq.contiguous()).data_ptr(), p.const(dqv).data_ptr(), float(qs)))
+    chosen = list(range(len(idx)))
+
+    def switch(k, on):
+        for pi, p in enumerate(plans):
+            _switch(p.fp8_candidates[idx[k]][0], states[pi][k] if on else None)
+
     if fraction < 1.0:
         if head is None:
             raise ValueError("mixed fp8 selection needs the head outputs (head=...)")
@@ -72,25 +108,23 @@ def enable_fp8(plan, run_calibration, select=None, fraction=1.0, head=None) -> i
             return sum((a.float() - r).abs().mean().item() for a, r in zip(head(), ref))
 
         sens = []
-        for (d, _, _), st in zip(cands, states):
-            _switch(d, st)
+        for k in range(len(idx)):
+            switch(k, True)
             sens.append(err())
-            _switch(d, None)
-        order.sort(key=lambda i: sens[i])
-        macs = [w.shape[0] * w.shape[1] * x.n * x.h * x.w for (_, x, w) in cands]
-        budget, used, chosen = fraction * sum(macs), 0.0, []
-        for i in order:
-            if used + macs[i] > budget + 1e-9:
-                continue
-            chosen.append(i)
-            used += macs[i]
-        order = chosen
-        plan.fp8_sensitivity = sens
-    for i in order:
-        _switch(cands[i][0], states[i])
-    plan.fp8_enabled = True
-    plan.fp8_switched = sorted(order)
-    return len(order)
+            switch(k, False)
+        macs = [candidate_macs(plans[0].fp8_candidates[i]) for i in idx]
+        chosen, frac = select_by_mac_budget(sens, macs, fraction)
+        for p in plans:
+            p.fp8_sensitivity, p.fp8_mac_fraction = sens, frac
+    else:
+        for p in plans:
+            p.fp8_mac_fraction = 1.0
+    for k in chosen:
+        switch(k, True)
+    for p in plans:
+        p.fp8_enabled = True
+        p.fp8_switched = sorted(idx[k] for k in chosen)
+    return len(chosen)
 
 
 def e4m3_round(t: torch.Tensor) -> torch.Tensor:
