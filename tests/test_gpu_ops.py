@@ -1012,3 +1012,63 @@ def test_golden_nms_from_fixture(golden_dir):
     for i in range(2):
         assert np.array_equal(pred[i].cpu().numpy(), g[f"pred{i}"])
         assert np.array_equal(val[i].cpu().numpy(), g[f"val{i}"])
+
+
+@pytest.mark.parametrize("case", [
+    # (kind, cin, cout, k, s, shape, residual, sliced): every dsc_lean.hip instantiation, ragged maps, channel slices
+    ("ds", 64, 64, 3, 1, (16, 64, 40, 40), False, False), ("ds", 64, 64, 7, 1, (16, 64, 40, 40), True, False),
+    ("ds", 64, 64, 3, 1, (3, 64, 13, 21), True, True), ("ds", 64, 64, 7, 1, (2, 64, 9, 30), True, True),
+    ("ds", 128, 128, 3, 1, (4, 128, 20, 20), True, False), ("ds", 128, 128, 7, 1, (4, 128, 20, 20), True, True),
+    ("ds", 128, 128, 3, 2, (2, 128, 80, 80), False, False), ("ds", 128, 256, 3, 2, (2, 128, 40, 40), False, True),
+    ("ds", 128, 128, 3, 2, (1, 128, 19, 27), False, False),
+    ("pair", 64, 64, 3, 1, (2, 64, 80, 80), False, False), ("pair", 128, 64, 3, 1, (2, 128, 40, 40), False, True),
+    ("pair", 256, 64, 3, 1, (2, 256, 20, 20), False, False), ("tail", 64, 64, 3, 1, (3, 64, 40, 40), False, False),
+    ("tail", 64, 64, 3, 1, (1, 64, 11, 13), False, True),
+])
+def test_dsconv_lean_bit_identical(case, monkeypatch):
+    """dsc_lean.hip (one global round trip, all channels per workgroup) == dsconv.hip's chunked kernel, bit for
+    bit (same roundings, same tap and k-step orders), on DSConv (+ the DSBottleneck residual), the stride-2
+    DSConvs and the Detect DWConv -> Conv1x1 pairs (+ the class-conv tail); and close to the oracle."""
+    from oracle import model as om
+    from ydbl import _lib
+    from ydbl.nn import modules as M
+    from ydbl.utils.synthetic import trained_like_
+
+    kind, cin, cout, k, s, shape, residual, sliced = case
+    torch.manual_seed(cin * 7 + cout + k + shape[2])
+    x = torch.randn(*shape)
+    if kind == "ds":
+        o = trained_like_(om.DSConv(cin, cout, k, s), seed=k).eval()
+    else:
+        o = trained_like_(torch.nn.Sequential(om.DWConv(cin, cin, k), om.Conv(cin, cout, 1)), seed=k).eval()
+    cls = torch.nn.Conv2d(cout, 3, 1) if kind == "tail" else None
+    ho, wo = (shape[2] + 2 * (k // 2) - k) // s + 1, (shape[3] + 2 * (k // 2) - k) // s + 1
+    r = torch.randn(shape[0], cout, ho, wo) if residual else None
+    outs = []
+    for lean in ("1", "0"):
+        monkeypatch.setenv("YDBL_DS_LEAN", lean)
+        plan = _plan(torch.float16)
+        xv = _tv_from_nchw(plan, x, cs_extra=8 if sliced else 0, c_off=8 if sliced else 0)
+        rv = _tv_from_nchw(plan, r, cs_extra=16 if sliced else 0, c_off=16 if sliced else 0) if residual else None
+        ybuf = plan.alloc(shape[0], ho, wo, cout + (32 if sliced else 0))
+        yv = ybuf.cslice(16, cout) if sliced else ybuf
+        tv = plan.alloc(shape[0], ho, wo, 3) if cls is not None else None
+        if kind == "ds":
+            pm = M.DSConv(cin, cout, k, s)
+            pm.load_state_dict(o.state_dict())
+            pm.emit(plan, xv, yv, res=rv, res_mode=_lib.RES_ADD if residual else _lib.RES_NONE)
+        else:
+            dwc, pwc = M.DWConv(cin, cin, k), M.Conv(cin, cout, 1)
+            dwc.load_state_dict(o[0].state_dict())
+            pwc.load_state_dict(o[1].state_dict())
+            _, done = M.emit_dw_pw(plan, dwc, pwc, xv, yv, tail_conv=cls, tail_out=tv)
+            assert done == (cls is not None)
+        assert [st.fn.__name__ for st in plan.steps] == ["ydbl_dsconv_nhwc"]
+        _run(plan)
+        outs.append((yv.nchw().float().cpu(), tv.nchw().float().cpu() if tv is not None else None))
+    assert torch.equal(outs[0][0], outs[1][0]), (outs[0][0] - outs[1][0]).abs().max()
+    if cls is not None:
+        assert torch.equal(outs[0][1], outs[1][1])
+    with torch.no_grad():
+        ref = o(x) + (r if residual else 0)
+    torch.testing.assert_close(outs[0][0], ref, rtol=3e-2, atol=3e-2)

@@ -73,6 +73,9 @@ template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s);
 // conv3x3.hip: fp16 3x3 stride-1 convs with Cin 32..128 and VGPR-resident weights.
 bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s);
+// dsc_lean.hip: one-round-trip DSConv / DWConv->Conv1x1 for the small-map shapes it is built for.
+bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, int k, int st, int dil,
+                  hipStream_t s);
 
 template <typename T>
 __device__ __forceinline__ f32x4 mfma_chunk(const typename Vec<T>::type& a, const typename Vec<T>::type& b, f32x4 c);

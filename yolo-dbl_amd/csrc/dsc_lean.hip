@@ -1,0 +1,256 @@
+// DSConv (U/nn/modules/conv.py:91-108: SiLU(BN(pw1x1(dw_kxk(x))))) and the Detect head's DWConv -> Conv1x1
+// pairs (U/nn/modules/head.py:93-101) for the small maps of the neck and head (20^2..80^2 at 640), laid
+// out for latency instead of streaming.
+//
+// At DBL-n's bs16 sub-batch sizes a DSConv layer moves 3-7 MB: one launch of dsconv.hip's chunked kernel
+// (halo of 32 channels at a time, three barriers and one global round trip per chunk, residual loaded in
+// the epilogue) spends most of its 10-15 us waiting on serial global latencies.  Here a workgroup owns an
+// 8x8 (or 4x8) output tile and ALL input channels:
+//   1. one round trip: the whole fp16 halo (every channel), the fp32 taps, then the pointwise weights'
+//      MFMA A fragments and the residual tile are issued together; the halo and taps land in LDS
+//      (fp16 halo: half the LDS bytes of an fp32 staging), the A fragments and residual stay in VGPRs;
+//   2. depthwise: thread = (channel quad, output row, CSEG-pixel segment) with a sliding register
+//      window per input row, fp32 FMAs in the reference's (ky, kx) tap order, optional DWConv bias +
+//      activation, rounded to fp16 into the MFMA B tile of all channels;
+//   3. pointwise on MFMA 16x16x32 over all k-steps, + bias, activation, residual, NHWC store (and the
+//      Detect class conv tail of conv_common.hpp when one wave holds all 64 output channels).
+// Two barriers per launch.  Every rounding and every accumulation order is dsconv.hip's (taps and halo
+// rounded to the activation dtype, k-steps in channel order), so the outputs are bit-identical to it
+// (tests/test_gpu_ops.py::test_dsconv_lean_bit_identical).
+#include <stdlib.h>
+
+#include "conv_common.hpp"
+
+namespace ydbl {
+
+__device__ __forceinline__ int lean_bswz(int row, int kv) { return row * 4 + (kv ^ (((row >> 2) & 1) << 1)); }
+
+template <int C, int CO, int K, int S, int TH, int TW, int NT>
+__global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, const float* __restrict__ dww,
+                                                          const float* __restrict__ dwb, int dw_act, int tiles_x,
+                                                          int tiles_y, int ntiles) {
+  using T = _Float16;
+  constexpr int WAVES = NT / 64;
+  constexpr int CV = C / 8;                          // 16-byte vectors per pixel
+  constexpr int NQ = C / 4;                          // channel quads
+  constexpr int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K;
+  constexpr int IWP = IW | 1;                        // odd pixel pitch: rows r, r+1 in opposite bank halves
+  constexpr int HV = IH * IW * CV;
+  constexpr int HIT = (HV + NT - 1) / NT;
+  constexpr int CSEG = NQ * TH * TW / NT;            // outputs per depthwise task
+  static_assert(CSEG >= 1 && TW % CSEG == 0 && NQ * TH * (TW / CSEG) == NT, "depthwise task split");
+  constexpr int SEGW = (CSEG - 1) * S + K;
+  constexpr int TAPV = K * K * NQ;
+  constexpr int TIT = (TAPV + NT - 1) / NT;
+  constexpr int NPX = TH * TW, NTP = NPX / 16;       // 16-pixel MFMA tiles
+  static_assert(NPX % 16 == 0, "tile");
+  constexpr int NKS = C / 32;                        // pointwise k-steps
+  constexpr int NTC = CO / 16;                       // output-channel tiles
+  // per wave: a group of TN output-channel tiles (<= 64 channels; fewer for deep inputs, whose A fragments
+  // [TN][NKS] would not fit the VGPRs); all 64 when CO = 64 and C <= 128 (the Detect class-conv tail needs them)
+  constexpr int TNA = 16 / NKS < 1 ? 1 : 16 / NKS;
+  constexpr int TN = NTC < (TNA < 4 ? TNA : 4) ? NTC : (TNA < 4 ? TNA : 4);
+  constexpr int NCG = NTC / TN;
+  static_assert(NTC % TN == 0 && WAVES % NCG == 0, "channel groups over waves");
+  constexpr int WPG = WAVES / NCG;
+  constexpr int TM = (NTP + WPG - 1) / WPG;          // pixel tiles per wave
+  __shared__ h4 s_x[IH * IWP * NQ];                  // fp16 halo, [row][col][quad]
+  __shared__ f32x4 s_w[TAPV];                        // fp32 taps (rounded to fp16), [tap][quad]
+  __shared__ h8 s_b[NKS * NPX * 4];                  // pointwise B tile, [k-step][pixel][slot]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  int bid = xcd_remap(blockIdx.x, ntiles);
+  const int tx = bid % tiles_x;
+  bid /= tiles_x;
+  const int ty = bid % tiles_y;
+  const int b = bid / tiles_y;
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - p.PAD, ix0 = ox0 * S - p.PAD;
+
+  // ---- 1. one round trip: halo + taps (-> LDS), then A fragments + residual (-> VGPRs)
+  h8 xr[HIT];
+#pragma unroll
+  for (int it = 0; it < HIT; ++it) {
+    const int i = min(tid + it * NT, HV - 1);
+    const int cv = i % CV, px = i / CV;
+    const int hy = px / IW, hx = px - hy * IW;
+    const int iy = iy0 + hy, ix = ix0 + hx;
+    const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+    xr[it] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + cv * 8, p.x, ok);
+  }
+  f32x4 wr[TIT];
+#pragma unroll
+  for (int it = 0; it < TIT; ++it) {
+    const int i = min(tid + it * NT, TAPV - 1);
+    const f32x4 w = *reinterpret_cast<const f32x4*>(dww + (i / NQ) * C + (i % NQ) * 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) wr[it][e] = float(T(w[e]));  // the reference's .half() weights
+  }
+  const int cg = wave % NCG, wp = wave / NCG;
+  int co[TN];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) co[i] = (cg * TN + i) * 16 + 4 * g;  // this lane's 4 epilogue channels
+  int64_t pp[TM];
+  bool pv[TM];
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    const int pt = wp + WPG * j;
+    const int op = pt * 16 + r16;
+    const int oy = oy0 + op / TW, ox = ox0 + op % TW;
+    pv[j] = pt < NTP && oy < p.Ho && ox < p.Wo;
+    pp[j] = pv[j] ? ((int64_t)b * p.Ho + oy) * p.Wo + ox : 0;
+  }
+#pragma unroll
+  for (int it = 0; it < HIT; ++it) {
+    const int i = tid + it * NT;
+    if (i < HV) {
+      const int cv = i % CV, px = i / CV;
+      const int hy = px / IW, hx = px - hy * IW;
+      *reinterpret_cast<h8*>(&s_x[(hy * IWP + hx) * NQ + cv * 2]) = xr[it];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < TIT; ++it)
+    if (tid + it * NT < TAPV) s_w[tid + it * NT] = wr[it];
+  h8 af[TN][NKS];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) {
+    const int row = (cg * TN + i) * 16 + r16;  // A rows: output channel of this lane
+#pragma unroll
+    for (int m = 0; m < NKS; ++m) af[i][m] = vload(p.w + (int64_t)row * p.KPAD + m * 32 + g * 8);
+  }
+  h4 rv[TN][TM];
+  if (p.res != YDBL_RES_NONE) {
+#pragma unroll
+    for (int j = 0; j < TM; ++j)
+#pragma unroll
+      for (int i = 0; i < TN; ++i) rv[i][j] = *reinterpret_cast<const h4*>(p.r + pp[j] * p.rcs + co[i]);
+  }
+  __syncthreads();
+
+  // ---- 2. depthwise: task = (quad q, output row r, segment sg), quad fastest
+  {
+    const int q = tid % NQ;
+    const int r = (tid / NQ) % TH;
+    const int sg = tid / (NQ * TH);
+    float a[CSEG][4];
+#pragma unroll
+    for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[c][e] = 0.f;
+    constexpr int KU = K <= 3 ? K : 1;  // the 7x7: one input row's window + taps live at a time
+#pragma unroll KU
+    for (int ky = 0; ky < K; ++ky) {
+      const h4* xrow = &s_x[((r * S + ky) * IWP + sg * CSEG * S) * NQ + q];
+      float xs[SEGW][4];
+#pragma unroll
+      for (int i = 0; i < SEGW; ++i) {
+        const h4 v = xrow[i * NQ];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xs[i][e] = float(v[e]);
+      }
+      f32x4 wv[K];
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) wv[kx] = s_w[(ky * K + kx) * NQ + q];
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+        for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[c][e] = fmaf(xs[c * S + kx][e], wv[kx][e], a[c][e]);
+    }
+    if (dwb) {  // uniform: DWConv (+ folded BN) bias and activation before the pointwise
+      const f32x4 bq = *reinterpret_cast<const f32x4*>(dwb + q * 4);
+#pragma unroll
+      for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[c][e] = apply_act<T>(a[c][e] + bq[e], dw_act);
+    }
+    const int ks = q / 8, ql = q % 8;  // k-step and 4-channel slot of this quad
+#pragma unroll
+    for (int c = 0; c < CSEG; ++c) {
+      const int px = r * TW + sg * CSEG + c;
+      *(reinterpret_cast<h4*>(&s_b[ks * NPX * 4 + lean_bswz(px, ql >> 1)]) + (ql & 1)) = to_h4_rne(a[c]);
+    }
+  }
+  __syncthreads();
+
+  // ---- 3. pointwise MFMA over all k-steps, epilogue
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int m = 0; m < NKS; ++m)
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      const int pt = wp + WPG * j;
+      if (TM * WPG == NTP || pt < NTP) {
+        const h8 bf = s_b[m * NPX * 4 + lean_bswz(pt * 16 + r16, g)];
+#pragma unroll
+        for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][m], bf, acc[i][j], 0, 0, 0);
+      }
+    }
+  float bv[TN][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i) load_f<4>(p.bias + co[i], bv[i]);
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    if (!pv[j]) continue;
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      float v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] + bv[i][q], p.act);
+      if (p.res == YDBL_RES_ADD) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) + v[q];
+      } else if (p.res == YDBL_RES_MUL) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) * v[q];
+      }
+      store_f<4>(p.y + pp[j] * p.ycs + co[i], v);
+    }
+  }
+  if constexpr (NCG == 1 && TN == 4) {  // Detect class conv over the 64 output channels (host-checked CO == 64)
+    if (p.t3w) conv_tail_1x1<T, TN, TM>(p, acc, pp, pv, co, g);
+  }
+}
+
+template <int C, int CO, int K, int S, int TH, int TW, int NT>
+static void lean_go(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
+  const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
+  const int ntiles = a.N * tiles_y * tiles_x;
+  dsc_lean_kernel<C, CO, K, S, TH, TW, NT><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y, ntiles);
+}
+
+// Shapes built (DBL-n / DBL-s neck and head, fp16): DSBottleneck's k3 / k7 DSConvs at 64 / 128 channels, the
+// stride-2 DSConvs 128 -> 128 / 256, and the Detect DWConv -> Conv1x1 pairs (c_in 64 / 128 / 256 -> 64).
+bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, int k, int st, int dil,
+                  hipStream_t s) {
+XX
+  if ((off && *off == '0') || dil != 1 || a.y2) return false;
+  if (a.xcs % 8 || a.ycs % 4 || (a.res && a.rcs % 4) || a.KPAD != a.Cin) return false;
+  const int c = a.Cin, co = a.Cout;
+  if (a.t3w && co != 64) return false;
+  if (st == 1 && k == 3) {
+    if (c == 64 && co == 64) return lean_go<64, 64, 3, 1, 8, 8, 256>(a, dww, dwb, dw_act, s), true;
+    if (c == 128 && co == 128) return lean_go<128, 128, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
+    if (c == 128 && co == 64) return lean_go<128, 64, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
+    if (c == 256 && co == 64) return lean_go<256, 64, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
+  }
+  if (st == 1 && k == 7) {
+    if (c == 64 && co == 64) return lean_go<64, 64, 7, 1, 8, 8, 256>(a, dww, dwb, dw_act, s), true;
+    if (c == 128 && co == 128) return lean_go<128, 128, 7, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
+  }
+  if (st == 2 && k == 3 && c == 128) {
+    if (co == 128) return lean_go<128, 128, 3, 2, 4, 8, 512>(a, dww, dwb, dw_act, s), true;
+    if (co == 256) return lean_go<128, 256, 3, 2, 4, 8, 512>(a, dww, dwb, dw_act, s), true;
+  }
+  return false;
+}
+
+}  // namespace ydbl

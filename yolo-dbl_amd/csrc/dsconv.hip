@@ -236,6 +236,9 @@ static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, const float* 
 // double-buffered tile (more workgroups on the few pixels).
 template <typename T, int K, int S, int DIL>
 static int launch_ds(const ConvArgs<T>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
+  if constexpr (sizeof(T) == 2) {
+    if (try_dsc_lean(a, dww, dwb, dw_act, K, S, DIL, s)) return check_launch("ydbl_dsconv_nhwc");
+  }
   static const char* tv = getenv("YDBL_DS_TILE");  // A/B knob for scripts/ds_bench.py: 8 = 8x8 everywhere, S = 8x8 single-buffered
   const char t = tv && *tv ? tv[0] : 'A';
   // Fewer than 400 16x8 tiles (the bench's bs16 sub-batch graphs at 40^2: 240): 8x8 single-buffered
