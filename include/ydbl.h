@@ -39,7 +39,8 @@
  *   ydbl_pool_up_concat    <- FuseModule.forward block.py:1831-1840, DownsampleConv block.py:1927
  *   ydbl_dysample(_ex)     <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
  *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
- *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708
+ *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708 (ydbl_hg_fused: the whole
+ *                             AdaHGConv incl. pre_head_proj block.py:1645, one launch)
  *   ydbl_detect_decode     <- Detect._inference head.py:143-181 + DFL block.py:79-83 +
  *                             make_anchors/dist2bbox utils/tal.py:333-357 + NMS candidate
  *                             filter utils/ops.py:234-276
@@ -120,6 +121,15 @@ typedef struct {
   const float* tail_b;
   ydbl_view tail_y;
   int32_t tail_n;
+  /* optional trailing GEMM (C3's cv3 after its last bottleneck, nn/modules/block.py:259-273, for DSC3k
+   * block.py:1447-1503): g2_y[p] = g2_act(g2_w [y[p] ; g2_x[p]] + g2_b), y = this DSConv's output (after
+   * the residual), rounded to the view dtype, kept on chip and NOT stored.  g2_w [g2_y.c][y.c + g2_x.c] in
+   * the view dtype (k contiguous), g2_b fp32.  Built for fp16, k 7 stride 1, x.c == y.c == g2_x.c ==
+   * g2_y.c in {64, 128} (DSC3k2's DSC3k with e = 1); g2_w == NULL disables it. */
+  const void* g2_w;
+  const float* g2_b;
+  ydbl_view g2_x, g2_y;
+  int32_t g2_act;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 
@@ -212,12 +222,20 @@ typedef struct {
   const float* node_w;      /* [D][D] */
   const float* node_b;      /* [D] */
   void* workspace;          /* ydbl_hg_workspace() bytes */
+  const void* pre_w;        /* [D][D] pre_head_proj weight in x's dtype (ydbl_hg_fused only; else NULL) */
+  const float* pre_b;       /* [D] pre_head_proj bias (ydbl_hg_fused only) */
 } ydbl_hg_desc;
 int64_t ydbl_hg_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges);
 /* stage 1: context stats + prototypes (run before the xp GEMM or after; independent of xp) */
 int ydbl_hg_context(const ydbl_hg_desc* d, void* stream);
 /* stage 2: logits, softmax over tokens, vertex->edge->vertex, residual (needs xp) */
 int ydbl_hg_propagate(const ydbl_hg_desc* d, void* stream);
+/* The whole AdaHGConv (block.py:1582-1708, pre_head_proj included: xp unused, pre_w/pre_b set) in one launch,
+ * one 1024-thread workgroup per image with the N x E logits in LDS; head_dim 16, (dim, edges) in
+ * {64, 128} x {4, 8}, ydbl_hg_fused_lds() <= 160 KiB (else: ydbl_hg_context + conv + ydbl_hg_propagate).
+ * No workspace. */
+int64_t ydbl_hg_fused_lds(int32_t tokens, int32_t dim, int32_t edges, int32_t dtype);
+int ydbl_hg_fused(const ydbl_hg_desc* d, void* stream);
 
 /* Detect decode + NMS candidate extraction.
  * box[l]: fp32 view [n,h_l,w_l,64] (DFL logits), cls[l]: fp32 view [n,h_l,w_l,nc].

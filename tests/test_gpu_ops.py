@@ -723,11 +723,16 @@ def test_lskblock(dtype, c, h, w):
     # 16 heads), and a ragged N=257 (one token in the second workgroup)
     (64, 4, 2, 40, 40), (128, 8, 2, 40, 40), (256, 8, 1, 80, 80), (64, 4, 1, 1, 257),
 ])
-def test_c3ah_hypergraph(dtype, c, edges, n, h, w):
-    """AdaHyperedgeGen softmax over tokens (U/nn/modules/block.py:1652-1657) and AdaHGConv propagation."""
+@pytest.mark.parametrize("path", ["fused", "staged"])
+def test_c3ah_hypergraph(dtype, c, edges, n, h, w, path, monkeypatch):
+    """AdaHyperedgeGen softmax over tokens (U/nn/modules/block.py:1652-1657) and AdaHGConv propagation, through
+    the one-launch ydbl_hg_fused (where its LDS holds N x E logits: dim 64/128) and the staged
+    hg_context + pre_head_proj conv + hg_propagate path (YDBL_HG_UNFUSED)."""
     from oracle import model as om
     from ydbl.nn import modules as M
 
+    if path == "staged":
+        monkeypatch.setenv("YDBL_HG_UNFUSED", "1")
     torch.manual_seed(5)
     o = om.C3AH(c, c, 1, edges).eval()
     x = torch.randn(n, c, h, w)
@@ -1072,3 +1077,40 @@ def test_dsconv_lean_bit_identical(case, monkeypatch):
     with torch.no_grad():
         ref = o(x) + (r if residual else 0)
     torch.testing.assert_close(outs[0][0], ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("c,n,shape,sliced", [(64, 2, (16, 64, 40, 40), False), (64, 1, (3, 64, 13, 21), True),
+                                              (128, 2, (4, 128, 20, 20), True)])
+def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
+    """DSC3k (U/nn/modules/block.py:1447-1503, C3 with DSBottlenecks k3 -> k7, e = 1): cv3 as the trailing GEMM of
+    the last bottleneck's k7 DSConv (ydbl_dsconv_desc.g2: the bottleneck output stays on the CU) == the separate
+    k7 DSConv + cv3 launches, bit for bit; one launch fewer; close to the oracle."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+    from ydbl.utils.synthetic import trained_like_
+
+    torch.manual_seed(c + n + shape[2])
+    o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=c).eval()
+    x = torch.randn(*shape)
+    outs, nsteps = [], []
+    for fuse in ("1", ""):
+        if fuse:
+            monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
+        else:
+            monkeypatch.setenv("YDBL_NO_CV3_FUSE", "1")
+        pm = M.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7)
+        pm.load_state_dict(o.state_dict())
+        plan = _plan(torch.float16)
+        xv = _tv_from_nchw(plan, x)
+        ybuf = plan.alloc(shape[0], shape[2], shape[3], c + (24 if sliced else 0))
+        yv = ybuf.cslice(8, c) if sliced else ybuf
+        pm.emit(plan, xv, yv)
+        nsteps.append(len(plan.steps))
+        assert any("+cv3" in st.what for st in plan.steps) == bool(fuse)
+        _run(plan)
+        outs.append(yv.nchw().float().cpu())
+    assert nsteps[0] == nsteps[1] - 1
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+    with torch.no_grad():
+        ref = o(x)
+    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)

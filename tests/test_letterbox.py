@@ -1,6 +1,8 @@
 """LetterBox geometry and the oracle's cv2 INTER_LINEAR restatement (CPU); the GPU kernel vs the oracle
 (bit-exact) and the ndarray predict path (gpu)."""
 
+from pathlib import Path
+
 import numpy as np
 import pytest
 import torch
@@ -157,9 +159,10 @@ def test_predict_file_dir_glob_pil_sources(tmp_path):
     from PIL import Image
 
     from ydbl import YOLO
-    from ydbl.utils.synthetic import blob_images
+    from ydbl.utils.synthetic import blob_images, load_trained
 
     m = YOLO("yolov13n_DBL.yaml", nc=3)
+    load_trained(m.model, Path(__file__).resolve().parent / "golden" / "trained_yolov13n_DBL_nc3.npz")
     x = blob_images(2, 256, seed=11)
     frames = [np.ascontiguousarray((x[i].permute(1, 2, 0).numpy()[:, :, ::-1] * 255).round().astype(np.uint8))
               for i in range(2)]

@@ -26,6 +26,10 @@ struct ConvArgs {
   // y3[p][k] = sum_c t3w[k][c] * T(y[p][c]) + t3b[k]
   const float* t3w; const float* t3b;
   T* y3; int y3cs; int nt3;
+  // optional trailing GEMM over [y ; g2x] (dsc_lean.hip, C3's cv3): g2y = g2act(g2w [y ; g2x] + g2b), y not stored
+  const T* g2w; const float* g2b;
+  const T* g2x; int g2xcs;
+  T* g2y; int g2ycs; int g2act;
 };
 
 // ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------

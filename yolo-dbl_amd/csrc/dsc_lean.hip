@@ -25,7 +25,7 @@ namespace ydbl {
 
 __device__ __forceinline__ int lean_bswz(int row, int kv) { return row * 4 + (kv ^ (((row >> 2) & 1) << 1)); }
 
-template <int C, int CO, int K, int S, int TH, int TW, int NT>
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false>
 __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, const float* __restrict__ dww,
                                                           const float* __restrict__ dwb, int dw_act, int tiles_x,
                                                           int tiles_y, int ntiles) {
@@ -54,9 +54,15 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
   static_assert(NTC % TN == 0 && WAVES % NCG == 0, "channel groups over waves");
   constexpr int WPG = WAVES / NCG;
   constexpr int TM = (NTP + WPG - 1) / WPG;          // pixel tiles per wave
+  // TG: trailing GEMM over [y ; g2x] (2*CO channels, CO/16 output tiles as the pointwise): its B tile
+  // [2*CO/32 k-steps][pixel][slot] reuses the halo's LDS once the depthwise phase is over
+  constexpr int NKS2 = TG ? 2 * CO / 32 : 0;
+  static_assert(!TG || (C == CO && NKS2 * NPX * 4 * 16 <= IH * IWP * NQ * 8), "trailing GEMM layout");
+  constexpr int X2V = TG ? NPX * CO / 8 : 1, X2IT = (X2V + NT - 1) / NT;
   __shared__ h4 s_x[IH * IWP * NQ];                  // fp16 halo, [row][col][quad]
   __shared__ f32x4 s_w[TAPV];                        // fp32 taps (rounded to fp16), [tap][quad]
   __shared__ h8 s_b[NKS * NPX * 4];                  // pointwise B tile, [k-step][pixel][slot]
+  h8* s_g = reinterpret_cast<h8*>(s_x);              // TG: trailing GEMM B tile (after the depthwise phase)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -120,6 +126,17 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
     const int row = (cg * TN + i) * 16 + r16;  // A rows: output channel of this lane
 #pragma unroll
     for (int m = 0; m < NKS; ++m) af[i][m] = vload(p.w + (int64_t)row * p.KPAD + m * 32 + g * 8);
+  }
+  h8 x2r[X2IT];  // TG: the second GEMM input's tile (C3's cv2 branch), [pixel][8-channel vector]
+  if constexpr (TG) {
+#pragma unroll
+    for (int it = 0; it < X2IT; ++it) {
+      const int i = min(tid + it * NT, X2V - 1);
+      const int px = i / (CO / 8), cv = i % (CO / 8);
+      const int oy = oy0 + px / TW, ox = ox0 + px % TW;
+      const bool ok = oy < p.Ho && ox < p.Wo;
+      x2r[it] = vload_sel(p.g2x + (((int64_t)b * p.Ho + oy) * p.Wo + ox) * p.g2xcs + cv * 8, p.g2x, ok);
+    }
   }
   h4 rv[TN][TM];
   if (p.res != YDBL_RES_NONE) {
@@ -212,30 +229,91 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) * v[q];
       }
-      store_f<4>(p.y + pp[j] * p.ycs + co[i], v);
+      if constexpr (TG) {  // y (rounded as the unfused path stores it) -> the trailing GEMM's B tile
+        const int px = (wp + WPG * j) * 16 + r16, c = co[i];
+        *(reinterpret_cast<h4*>(&s_g[(c >> 5) * NPX * 4 + lean_bswz(px, (c >> 3) & 3)]) + ((c >> 2) & 1)) =
+            to_h4_rne(v);
+      } else {
+        store_f<4>(p.y + pp[j] * p.ycs + co[i], v);
+      }
     }
   }
-  if constexpr (NCG == 1 && TN == 4) {  // Detect class conv over the 64 output channels (host-checked CO == 64)
+  if constexpr (NCG == 1 && TN == 4 && !TG) {  // Detect class conv over the 64 output channels (host-checked CO == 64)
     if (p.t3w) conv_tail_1x1<T, TN, TM>(p, acc, pp, pv, co, g);
+  }
+  if constexpr (TG) {
+    // ---- 4. trailing GEMM: g2y = act(W2 [y ; g2x] + b2), K = 2*CO in channel order (the unfused cv3's k-steps)
+#pragma unroll
+    for (int it = 0; it < X2IT; ++it) {
+      const int i = tid + it * NT;
+      if (i < X2V) {
+        const int px = i / (CO / 8), cv = i % (CO / 8);
+        s_g[(CO / 32 + cv / 4) * NPX * 4 + lean_bswz(px, cv & 3)] = x2r[it];
+      }
+    }
+    h8 a2[TN][NKS2];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) {
+      const int row = (cg * TN + i) * 16 + r16;
+#pragma unroll
+      for (int m = 0; m < NKS2; ++m) a2[i][m] = vload(p.g2w + (int64_t)row * (2 * CO) + m * 32 + g * 8);
+    }
+    float b2v[TN][4];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) load_f<4>(p.g2b + co[i], b2v[i]);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int m = 0; m < NKS2; ++m)
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        const int pt = wp + WPG * j;
+        if (TM * WPG == NTP || pt < NTP) {
+          const h8 bf = s_g[m * NPX * 4 + lean_bswz(pt * 16 + r16, g)];
+#pragma unroll
+          for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i][m], bf, acc[i][j], 0, 0, 0);
+        }
+      }
+#pragma unroll
+    for (int j = 0; j < TM; ++j) {
+      if (!pv[j]) continue;
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] + b2v[i][q], p.g2act);
+        store_f<4>(p.g2y + pp[j] * p.g2ycs + co[i], v);
+      }
+    }
   }
 }
 
-template <int C, int CO, int K, int S, int TH, int TW, int NT>
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false>
 static void lean_go(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
   const int ntiles = a.N * tiles_y * tiles_x;
-  dsc_lean_kernel<C, CO, K, S, TH, TW, NT><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y, ntiles);
+  dsc_lean_kernel<C, CO, K, S, TH, TW, NT, TG><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y,
+                                                                               ntiles);
 }
 
 // Shapes built (DBL-n / DBL-s neck and head, fp16): DSBottleneck's k3 / k7 DSConvs at 64 / 128 channels, the
 // stride-2 DSConvs 128 -> 128 / 256, and the Detect DWConv -> Conv1x1 pairs (c_in 64 / 128 / 256 -> 64).
 bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, int k, int st, int dil,
                   hipStream_t s) {
-XX
+  const char* off = getenv("YDBL_DS_LEAN");  // A/B switch (read per launch: tests): 0 = dsconv.hip chunked kernel
   if ((off && *off == '0') || dil != 1 || a.y2) return false;
   if (a.xcs % 8 || a.ycs % 4 || (a.res && a.rcs % 4) || a.KPAD != a.Cin) return false;
   const int c = a.Cin, co = a.Cout;
   if (a.t3w && co != 64) return false;
+  if (a.g2w) {  // DSC3k's last bottleneck k7 DSConv + its cv3 (ydbl.h: g2)
+    if (st != 1 || k != 7 || c != co || a.g2xcs % 8 || a.g2ycs % 4) return false;
+    if (c == 64) return lean_go<64, 64, 7, 1, 8, 8, 256, true>(a, dww, dwb, dw_act, s), true;
+    if (c == 128) return lean_go<128, 128, 7, 1, 8, 8, 512, true>(a, dww, dwb, dw_act, s), true;
+    return false;
+  }
   if (st == 1 && k == 3) {
     if (c == 64 && co == 64) return lean_go<64, 64, 3, 1, 8, 8, 256>(a, dww, dwb, dw_act, s), true;
     if (c == 128 && co == 128) return lean_go<128, 128, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;

@@ -270,6 +270,17 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
     a.y3 = reinterpret_cast<T*>(d->tail_y.ptr); a.y3cs = d->tail_y.cs;
   }
   a.P = d->y.n * d->y.h * d->y.w;
+  if (d->g2_w) {  // trailing GEMM: only the lean kernel has it (ydbl.h: fp16, k 7 s 1, C 64 / 128)
+    a.g2w = reinterpret_cast<const T*>(d->g2_w); a.g2b = d->g2_b;
+    a.g2x = reinterpret_cast<const T*>(d->g2_x.ptr); a.g2xcs = d->g2_x.cs;
+    a.g2y = reinterpret_cast<T*>(d->g2_y.ptr); a.g2ycs = d->g2_y.cs; a.g2act = d->g2_act;
+    if constexpr (sizeof(T) == 2) {
+      if (d->k == 7 && d->stride == 1 && d->dil == 1 &&
+          try_dsc_lean(a, d->dw_w, d->dw_bias, d->dw_act, 7, 1, 1, s))
+        return check_launch("ydbl_dsconv_nhwc");
+    }
+    return fail(YDBL_EINVAL, "dsconv: the trailing GEMM (g2) needs fp16, k 7 stride 1, C 64 or 128 (lean kernel)");
+  }
   if (d->k == 3 && d->stride == 1 && d->dil == 1) return launch_ds<T, 3, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
   if (d->k == 3 && d->stride == 2 && d->dil == 1) return launch_ds<T, 3, 2, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
   if (d->k == 5 && d->stride == 1 && d->dil == 1) return launch_ds<T, 5, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
@@ -298,6 +309,13 @@ extern "C" int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream) {
     if (d->r.cs % 4 || d->r.dtype != d->y.dtype || d->r.n != d->y.n || d->r.h != d->y.h || d->r.w != d->y.w ||
         d->r.c < d->y.c)
       return fail(YDBL_EINVAL, "dsconv: residual shape mismatch");
+  }
+  if (d->g2_w) {
+    if (!d->g2_b || check_view(&d->g2_x, "dsconv.g2_x", true) || check_view(&d->g2_y, "dsconv.g2_y", false) ||
+        d->g2_x.c != d->y.c || d->g2_y.c != d->y.c || d->x.c != d->y.c || d->tail_w || d->g2_x.dtype != d->y.dtype ||
+        d->g2_y.dtype != d->y.dtype || d->g2_y.cs % 4 || d->g2_x.n != d->y.n || d->g2_x.h != d->y.h ||
+        d->g2_x.w != d->y.w || d->g2_y.n != d->y.n || d->g2_y.h != d->y.h || d->g2_y.w != d->y.w)
+      return fail(YDBL_EINVAL, "dsconv: g2 needs g2_x/g2_y of y's shape and dtype, x.c == y.c, no class tail");
   }
   if (d->tail_w) {
     if (!d->tail_b || d->tail_n < 1 || d->tail_n > 4 || d->y.c != 64 || d->res_mode != YDBL_RES_NONE ||

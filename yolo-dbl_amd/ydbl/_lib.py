@@ -45,7 +45,8 @@ class DsConvDesc(C.Structure):
                 ("bias", C.c_void_p), ("k", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32),
                 ("dil", C.c_int32), ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32),
                 ("dw_bias", C.c_void_p), ("dw_act", C.c_int32), ("tail_w", C.c_void_p), ("tail_b", C.c_void_p),
-                ("tail_y", View), ("tail_n", C.c_int32)]
+                ("tail_y", View), ("tail_n", C.c_int32), ("g2_w", C.c_void_p), ("g2_b", C.c_void_p),
+                ("g2_x", View), ("g2_y", View), ("g2_act", C.c_int32)]
 
 
 class DsBneckDesc(C.Structure):
@@ -58,7 +59,7 @@ class HgDesc(C.Structure):
     _fields_ = [("x", View), ("xp", View), ("y", View), ("num_edges", C.c_int32), ("num_heads", C.c_int32),
                 ("proto_base", C.c_void_p), ("ctx_w", C.c_void_p), ("ctx_b", C.c_void_p),
                 ("edge_w", C.c_void_p), ("edge_b", C.c_void_p), ("node_w", C.c_void_p), ("node_b", C.c_void_p),
-                ("workspace", C.c_void_p)]
+                ("workspace", C.c_void_p), ("pre_w", C.c_void_p), ("pre_b", C.c_void_p)]
 
 
 class DecodeDesc(C.Structure):
@@ -132,6 +133,8 @@ SIGNATURES = {
     "ydbl_hg_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_hg_context": ([C.POINTER(HgDesc), _P], C.c_int),
     "ydbl_hg_propagate": ([C.POINTER(HgDesc), _P], C.c_int),
+    "ydbl_hg_fused_lds": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_hg_fused": ([C.POINTER(HgDesc), _P], C.c_int),
     "ydbl_detect_decode": ([C.POINTER(DecodeDesc), _P], C.c_int),
     "ydbl_pred_candidates": ([C.POINTER(PredCandDesc), _P], C.c_int),
     "ydbl_nms_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),

@@ -163,10 +163,12 @@ def fused_dsconv_ok(dw: nn.Conv2d, x: TV, dtype) -> bool:
 def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Tensor, b_pw: torch.Tensor,
                 act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv",
                 w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE,
-                tail: tuple | None = None) -> TV:
+                tail: tuple | None = None, g2: tuple | None = None) -> TV:
     """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA.
     w_dw / b_dw / dw_act: folded DWConv weights, bias and activation (Detect's DWConv -> Conv1x1 pair).
-    tail = (w [n, co], b [n], out view): a trailing 1x1 conv with n <= 4 outputs in the same launch."""
+    tail = (w [n, co], b [n], out view): a trailing 1x1 conv with n <= 4 outputs in the same launch.
+    g2 = (w [co2, co + c2] fp32, b [co2], x2 view, y2 view, act): a trailing GEMM over [y ; x2] into y2 (C3's
+    cv3 after the last bottleneck); y itself is then not stored (include/ydbl.h, ydbl_dsconv_desc.g2)."""
     k, st, p, d = dw.kernel_size[0], dw.stride[0], dw.padding[0], dw.dilation[0]
     c = x.c
     co = w_pw.shape[0]
@@ -185,10 +187,16 @@ def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Te
         tw, tb = plan.const(tail[0].float().contiguous()), plan.const(tail[1].float().contiguous())
         tail_args = (tw.data_ptr(), tb.data_ptr(), tail[2].struct(), tail[2].c)
         what += "+1x1"
+    g2w = g2b = None
+    g2_args = (None, None, _null_view(), _null_view(), 0)
+    if g2 is not None:
+        g2w, g2b = plan.const(g2[0].float().to(plan.dtype).contiguous()), plan.const(g2[1].float().contiguous())
+        g2_args = (g2w.data_ptr(), g2b.data_ptr(), g2[2].struct(), g2[3].struct(), int(g2[4]))
+        what += "+cv3"
     desc = _lib.DsConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(),
                            dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode,
-                           dwb.data_ptr() if dwb is not None else None, dw_act, *tail_args)
-    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, dwb, tw, tb, desc])
+                           dwb.data_ptr() if dwb is not None else None, dw_act, *tail_args, *g2_args)
+    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, dwb, tw, tb, g2w, g2b, desc])
     return y
 
 
@@ -517,6 +525,10 @@ class C3(nn.Module):
             # cv2 and cv1 both read x: one launch into [m slot | cv2 | cv1] (cv3 reads the first 2c_)
             buf = plan.alloc(x.n, x.h, x.w, 3 * c_)
             emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
+            if self._cv3_fusable(plan, x):
+                # DSC3k: cv3 rides in the last DSBottleneck's k7 DSConv (its output never leaves the CU)
+                t = emit_seq(plan, list(self.m)[:-1], buf.cslice(2 * c_, c_)) if len(self.m) > 1 else buf.cslice(2 * c_, c_)
+                return self.m[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out))
             emit_seq(plan, self.m, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
             return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
         buf = plan.alloc(x.n, x.h, x.w, 2 * c_)
@@ -524,6 +536,23 @@ class C3(nn.Module):
         emit_seq(plan, self.m, t, buf.cslice(0, c_))
         self.cv2.emit(plan, x, buf.cslice(c_, c_))
         return self.cv3.emit(plan, buf, out)
+
+
+    def _cv3_fusable(self, plan, x) -> bool:
+        """cv3 can run as the trailing GEMM of the last bottleneck's k7 DSConv (dsc_lean.hip, ydbl_dsconv_desc.g2):
+        fp16, m = DSBottlenecks ending in a k7 stride-1 DSConv with c_ in {64, 128} in and out, cv3 a 1x1 SiLU
+        Conv 2c_ -> c_ (DSC3k with e = 1, U/nn/modules/block.py:1447-1503)."""
+        if plan.dtype != torch.float16 or os.environ.get("YDBL_NO_CV3_FUSE") or not len(self.m):
+            return False
+        last, c_ = self.m[-1], self.cv1.conv.out_channels
+        if not isinstance(last, DSBottleneck):
+            return False
+        dw, pw = last.cv2.dw, last.cv2.pw
+        c3 = self.cv3.conv
+        return (c_ in (64, 128) and dw.kernel_size == (7, 7) and dw.stride == (1, 1) and dw.dilation == (1, 1)
+                and dw.bias is None and dw.in_channels == pw.out_channels == c_ and last.cv1.pw.out_channels == c_
+                and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.groups == 1
+                and c3.in_channels == 2 * c_ and c3.out_channels == c_ and isinstance(self.cv3.act, nn.SiLU))
 
 
 class GhostBottleneck(nn.Module):
@@ -580,8 +609,20 @@ class DSBottleneck(nn.Module):
                 and a.dw.bias is None and b.dw.bias is None and x.cs % 8 == 0 and y.cs % 8 == 0
                 and (y.base is not x.base or y.off + y.c <= x.off or x.off + x.c <= y.off))
 
-    def emit(self, plan, x, out=None):
+    def emit(self, plan, x, out=None, cv3=None):
+        """cv3 = (C3's cv3 Conv, its second input view (the cv2 branch), its output view or None): the DSC3k's
+        cv3 as the trailing GEMM of this bottleneck's k7 DSConv; returns cv3's output then."""
         y = out if out is not None else plan.alloc(x.n, x.h, x.w, self.cv2.pw.out_channels)
+        if cv3 is not None:
+            conv3, x2, o3 = cv3
+            o3 = o3 if o3 is not None else plan.alloc(x.n, x.h, x.w, conv3.conv.out_channels)
+            t = self.cv1.emit(plan, x)
+            w, b = fold_bn(self.cv2.pw.weight, self.cv2.pw.bias, self.cv2.bn)
+            w3, b3 = conv3.folded()
+            emit_dsconv(plan, self.cv2.dw, t, y, w, b, _lib.ACT_SILU, x if self.add else None,
+                        _lib.RES_ADD if self.add else _lib.RES_NONE,
+                        g2=(w3.reshape(w3.shape[0], -1), b3, x2, o3, _act_code(conv3.act)))
+            return o3
         if self.fused_ok(plan, x, y):
             keep = []
 
@@ -662,15 +703,25 @@ class AdaHGConv(nn.Module):
         g = self.edge_generator
         D, E = x.c, g.num_hyperedges
         y = out if out is not None else plan.alloc(x.n, x.h, x.w, D)
+        c = plan.const
+        p = [c(g.prototype_base.float()), c(g.context_net.weight.float()), c(g.context_net.bias.float()),
+             c(self.edge_proj[0].weight.float()), c(self.edge_proj[0].bias.float()),
+             c(self.node_proj[0].weight.float()), c(self.node_proj[0].bias.float())]
+        lds = _lib.lib.ydbl_hg_fused_lds(x.h * x.w, D, E, _lib.dtype_code(plan.dtype))
+        if (not os.environ.get("YDBL_HG_UNFUSED") and D == 16 * g.num_heads and 0 < lds <= 159 * 1024
+                and x.c == D and (y.base is not x.base or y.off + y.c <= x.off or x.off + x.c <= y.off)):
+            # the whole AdaHGConv, pre_head_proj included, in one launch per call (csrc/hg_fused.hip)
+            pw = c(g.pre_head_proj.weight.detach().float().to(plan.dtype).contiguous())
+            pb = c(g.pre_head_proj.bias.detach().float())
+            d = HgDesc(x.struct(), _null_view(), y.struct(), E, g.num_heads, *[t.data_ptr() for t in p], None,
+                       pw.data_ptr(), pb.data_ptr())
+            plan.launch("ydbl_hg_fused", d, what="AdaHG.fused", keep=[d, pw, pb, *p])
+            return y
         # X_proj = pre_head_proj(X) as a 1x1 conv over the token grid
         xp = plan.alloc(x.n, x.h, x.w, D)
         emit_dense(plan, x, xp, g.pre_head_proj.weight.detach().float().cpu().view(D, D, 1, 1),
                    g.pre_head_proj.bias.detach().float().cpu(), what="AdaHG.pre_proj")
         ws = plan.scratch(_lib.lib.ydbl_hg_workspace(x.n, x.h * x.w, D, E))
-        c = plan.const
-        p = [c(g.prototype_base.float()), c(g.context_net.weight.float()), c(g.context_net.bias.float()),
-             c(self.edge_proj[0].weight.float()), c(self.edge_proj[0].bias.float()),
-             c(self.node_proj[0].weight.float()), c(self.node_proj[0].bias.float())]
         d = HgDesc(x.struct(), xp.struct(), y.struct(), E, g.num_heads, *[t.data_ptr() for t in p], ws.data_ptr())
         plan.launch("ydbl_hg_context", d, what="AdaHG.context", keep=[d, ws, *p])
         plan.launch("ydbl_hg_propagate", d, what="AdaHG.propagate", keep=[d])
