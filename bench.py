@@ -64,7 +64,11 @@ def dsconv_traffic(step, elsize):
         byts += _px(y) * y.c * elsize
     if d.tail_w:
         byts += _px(y) * d.tail_n * elsize
-    return byts, 2.0 * _px(y) * x.c * (d.k * d.k + y.c)
+    flops = 2.0 * _px(y) * x.c * (d.k * d.k + y.c)
+    if d.g2_w:  # trailing GEMM (C3's cv3): y stays on chip; the cv2 branch is read and cv3's output written
+        byts += (_px(d.g2_x) * d.g2_x.c + _px(d.g2_y) * d.g2_y.c - _px(y) * y.c) * elsize
+        flops += 2.0 * _px(d.g2_y) * d.g2_y.c * (y.c + d.g2_x.c)
+    return byts, flops
 
 
 def bneck_traffic(step, elsize):
@@ -145,7 +149,24 @@ def other_traffic(step, elsize):
     return 0.0, 0.0
 
 
+def dysample2_traffic(step, elsize):
+    """ydbl_dysample2: x read once (offset conv and sample), the 2x-upsampled y written (+ FullPAD second output)."""
+    d = step.args[0]
+    byts = (_px(d.x) * d.x.c + _px(d.y) * d.y.c) * elsize
+    if d.y2.ptr:
+        byts += 2 * _px(d.y) * d.y.c * elsize
+    return byts, 2.0 * _px(d.x) * d.x.c * 8 * d.groups
+
+
+def hg_fused_traffic(step, elsize):
+    """ydbl_hg_fused: the tokens X read once, y written once (the pre_head_proj xp never leaves the CU)."""
+    d = step.args[0]
+    n, dd, e = _px(d.x), d.x.c, d.num_edges
+    return 2 * n * dd * elsize, 2.0 * n * (dd * dd + 3 * e * dd) + 2.0 * d.x.n * e * dd * (2 * dd + 2 * dd)
+
+
 TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("dsconv", dsconv_traffic),
+           "ydbl_dysample2": ("dysample", dysample2_traffic), "ydbl_hg_fused": ("hypergraph", hg_fused_traffic),
            "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
            "ydbl_dsbottleneck_nhwc": ("dsbottleneck", dsbneck_traffic),
            "ydbl_dysample_ex": ("dysample", dysample_traffic)}

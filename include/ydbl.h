@@ -38,6 +38,7 @@
  *   ydbl_gate_add          <- FullPAD_Tunnel.forward nn/modules/block.py:1954-1956
  *   ydbl_pool_up_concat    <- FuseModule.forward block.py:1831-1840, DownsampleConv block.py:1927
  *   ydbl_dysample(_ex)     <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
+ *   ydbl_dysample2         <- DySample.forward DySample.py:63-81 (offset conv + sample, one launch)
  *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
  *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708 (ydbl_hg_fused: the whole
  *                             AdaHGConv incl. pre_head_proj block.py:1645, one launch)
@@ -200,6 +201,19 @@ typedef struct {
   float a2, b2;
 } ydbl_dysample_desc;
 int ydbl_dysample_ex(const ydbl_dysample_desc* d, void* stream);
+/* The whole DySample forward (DySample.py:48-81: offset conv + grid_sample) in one launch: off_w [8*groups][c]
+ * in x's dtype holds the offset conv weights * 0.25 (K contiguous), off_b fp32 [8*groups] = 0.25 * bias +
+ * init_pos (both folds exact); the offsets are rounded to x's dtype as the two-launch path stores them, and the
+ * result is bit-identical to ydbl_conv2d_nhwc + ydbl_dysample_ex.  groups = 4, c / groups in {16, 32, 64}. */
+typedef struct {
+  ydbl_view x;
+  const void* off_w;
+  const float* off_b;
+  int32_t groups;
+  ydbl_view y, y2, r2;
+  float a2, b2;
+} ydbl_dysample2_desc;
+int ydbl_dysample2(const ydbl_dysample2_desc* d, void* stream);
 
 /* LSKblock gate: attn view = [a1 | a2] (2*half channels, each half = dim/2);
  * agg = [mean_c, max_c](attn); sig = sigmoid(conv7x7(agg) + sb); out = a1*sig0 + a2*sig1.

@@ -94,7 +94,57 @@ def case_bneck(B, c, H):
     return f"bneck c{c}@{H} bs{B}", build
 
 
-CASES = [case_gate(16, 8, 8, 64), case_gate(16, 40, 40, 64),
+def case_stem2(B, S=640, c0=8):
+    def build():
+        p = Plan(torch.device("cuda"), torch.float16)
+        x = torch.rand(B, 3, S, S, device="cuda")
+        p.buffers.append(x)
+        m0, m1 = M.Conv(3, c0, 3, 1).eval(), M.Conv(c0, 2 * c0, 3, 2).eval()
+        M.emit_stem2(m0, m1, p, x, B, 3, S, S)
+        return p
+    return f"stem2 c0={c0}@{S} bs{B}", build
+
+
+def case_box3(B, cin, H):
+    def build():
+        p = Plan(torch.device("cuda"), torch.float16)
+        x = p.alloc(B, H, H, cin)
+        rnd(p, x)
+        seq = torch.nn.Sequential(M.Conv(cin, 64, 3), M.Conv(64, 64, 3), torch.nn.Conv2d(64, 64, 1)).eval()
+        out = p.alloc(B, H, H, 67)
+        assert M.emit_detect_box(p, seq, x, out.cslice(0, 64))
+        return p
+    return f"box3 {cin}@{H} bs{B}", build
+
+
+def case_pair(B, cin, co, H, tail=False):
+    def build():
+        p = Plan(torch.device("cuda"), torch.float16)
+        x = p.alloc(B, H, H, cin)
+        rnd(p, x)
+        dwc, pwc = M.DWConv(cin, cin, 3).eval(), M.Conv(cin, co, 1).eval()
+        lv = p.alloc(B, H, H, co + 3)
+        cls = torch.nn.Conv2d(co, 3, 1) if tail else None
+        M.emit_dw_pw(p, dwc, pwc, x, lv.cslice(0, co) if tail else None, tail_conv=cls,
+                     tail_out=lv.cslice(co, 3) if tail else None)
+        return p
+    return f"pair {cin}->{co}{'+tail' if tail else ''}@{H} bs{B}", build
+
+
+def case_dysample(B, c, H):
+    def build():
+        p = Plan(torch.device("cuda"), torch.float16)
+        x = p.alloc(B, H, H, c)
+        rnd(p, x)
+        M.DySample(c).emit(p, x)
+        return p
+    return f"dysample {c}@{H} bs{B}", build
+
+
+CASES = [case_dysample(16, 128, 40), case_dysample(16, 256, 20), case_stem2(16), case_box3(16, 64, 80), case_box3(16, 128, 40), case_pair(16, 64, 64, 80),
+         case_pair(16, 64, 64, 80, True), case_pair(16, 128, 64, 40), case_pair(16, 256, 64, 20),
+         case_dsconv(16, 128, 128, 3, 2, 80, 80), case_conv(16, 16, 32, 3, 2, 320, 320),
+         case_conv(16, 32, 64, 3, 2, 160, 160), case_bneck(16, 32, 160),case_gate(16, 8, 8, 64), case_gate(16, 40, 40, 64),
          case_dsconv(16, 64, 64, 3, 1, 40, 40), case_dsconv(16, 64, 64, 7, 1, 40, 40, res=True),
          case_dsconv(16, 128, 128, 3, 1, 20, 20), case_dsconv(16, 128, 128, 7, 1, 20, 20, res=True),
          case_conv(16, 128, 64, 1, 1, 40, 40), case_conv(16, 64, 128, 1, 1, 40, 40), case_conv(16, 256, 128, 1, 1, 20, 20),
@@ -103,11 +153,21 @@ CASES = [case_gate(16, 8, 8, 64), case_gate(16, 40, 40, 64),
 
 
 def main():
-    sel = sys.argv[1:]
+    eager = 0
+    sel = [a for a in sys.argv[1:] if not a.startswith("--eager")]
+    for a in sys.argv[1:]:
+        if a.startswith("--eager="):
+            eager = int(a.split("=")[1])  # rocprofv3 mode: plain eager runs of each selected plan
     for name, build in CASES:
         if sel and not any(s in name for s in sel):
             continue
         plan = build()
+        if eager:
+            for _ in range(eager):
+                plan.run()
+            torch.cuda.synchronize()
+            print(f"{name:40s} ran {eager}x eager", flush=True)
+            continue
         print(f"{name:40s} {graph_us(plan):8.2f} us/launch in graph", flush=True)
 
 

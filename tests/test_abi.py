@@ -46,6 +46,7 @@ STRUCTS = {
     "ydbl_bottleneck_desc": "BottleneckDesc",
     "ydbl_dsbneck_desc": "DsBneckDesc",
     "ydbl_dysample_desc": "DySampleDesc",
+    "ydbl_dysample2_desc": "DySample2Desc",
 }
 
 

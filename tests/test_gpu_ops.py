@@ -1114,3 +1114,41 @@ def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
     with torch.no_grad():
         ref = o(x)
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("c,shape,spread,fullpad", [(128, (16, 128, 40, 40), 0.01, False), (256, (4, 256, 20, 20), 0.01, True),
+                                                    (64, (2, 64, 13, 17), 0.3, True), (128, (3, 128, 9, 40), 1.0, False)])
+def test_dysample_fused_bit_identical(dtype, c, shape, spread, fullpad, monkeypatch):
+    """ydbl_dysample2 (offset conv + sample in one launch, the group's tile + 2-px halo in LDS, global fallback
+    for corners outside it) == ydbl_conv2d_nhwc + ydbl_dysample_ex, bit for bit, with small (in-window) and
+    large (border-clamped, out-of-window) offsets, and with the fused FullPAD second output."""
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(c + shape[2])
+    ds = M.DySample(c)
+    with torch.no_grad():
+        ds.offset.weight.normal_(0, spread)
+        ds.offset.bias.normal_(0, 10 * spread)
+    x = torch.randn(*shape)
+    r = torch.randn(shape[0], c, 2 * shape[2], 2 * shape[3])
+    outs = []
+    for fused in ("", "1"):
+        if fused:
+            monkeypatch.delenv("YDBL_DS2_OFF", raising=False)
+        else:
+            monkeypatch.setenv("YDBL_DS2_OFF", "1")
+        plan = _plan(dtype)
+        xv = _tv_from_nchw(plan, x)
+        y = ds.emit(plan, xv)
+        assert ("DySample.fused" in [st.what for st in plan.steps]) == bool(fused)
+        y2 = None
+        if fullpad:
+            rv = _tv_from_nchw(plan, r)
+            y2 = plan.alloc(shape[0], 2 * shape[2], 2 * shape[3], c)
+            assert plan.fuse_second_output(plan.writer_of(y), y2, rv, 0.7, 1.0) is not None
+        _run(plan)
+        outs.append((y.nchw().float().cpu(), y2.nchw().float().cpu() if y2 is not None else None))
+    assert torch.equal(outs[0][0], outs[1][0]), (outs[0][0] - outs[1][0]).abs().max()
+    if fullpad:
+        assert torch.equal(outs[0][1], outs[1][1])

@@ -126,6 +126,27 @@ __device__ __forceinline__ h4 to_h4_rne(const float* a) {
   return h4{(_Float16)v0, (_Float16)v1, (_Float16)v2, (_Float16)v3};
 }
 
+// Explicit-contraction arithmetic for results two kernels must agree on bit for bit.  Under hipcc's
+// default fp-contract=fast the backend fuses a*b + c into an fma or not per kernel and even per
+// element (register pressure, v_fma_mix selection), so the same source expression in two kernels
+// can differ by an ulp.  These fix the rounding points.
+// FullPAD_Tunnel mix y2 = a2 * y + b2 * r, equal to ydbl_gate_add's fmaf(gate, b, a) when one of the
+// two coefficients is 1 (the only way the fused second outputs use it: a2 = 1 or b2 = 1).
+__device__ __forceinline__ float pad_mix(float a2, float y, float b2, float r) {
+  if (b2 == 1.0f) return __builtin_fmaf(a2, y, r);
+  if (a2 == 1.0f) return __builtin_fmaf(b2, r, y);
+  return __builtin_fmaf(a2, y, b2 * r);
+}
+// bilinear blend in grid_sample's nw, ne, sw, se order, one rounding per term
+__device__ __forceinline__ float blend4(float vnw, float wnw, float vne, float wne, float vsw, float wsw, float vse,
+                                        float wse) {
+  float o = vnw * wnw;
+  asm volatile("" : "+v"(o));  // keep the first product a plain multiply
+  o = __builtin_fmaf(vne, wne, o);
+  o = __builtin_fmaf(vsw, wsw, o);
+  return __builtin_fmaf(vse, wse, o);
+}
+
 // v as a stored T would hold it, back in fp32 (T = _Float16: f16_rne; T = float: v)
 template <typename T>
 __device__ __forceinline__ float round_to(float v) {

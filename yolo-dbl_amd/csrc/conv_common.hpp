@@ -174,12 +174,12 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 
           load_f<4>(r2p, r2v);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            r2v[q] = p.a2 * round_to<T>(v[q]) + p.b2 * r2v[q];  // y as stored (rounded to T)
+            r2v[q] = pad_mix(p.a2, round_to<T>(v[q]), p.b2, r2v[q]);  // y as stored (rounded to T)
           }
           store_f<4>(y2p, r2v);
         } else {
           for (int q = 0; q < 4 && co[i] + q < p.Cout; ++q) {
-            const float o = p.a2 * round_to<T>(v[q]) + p.b2 * float(r2p[q]);
+            const float o = pad_mix(p.a2, round_to<T>(v[q]), p.b2, float(r2p[q]));
             store_f<1>(y2p + q, &o);
           }
         }

@@ -314,7 +314,7 @@ __global__ __launch_bounds__(256) void gate_add_kernel(DView<const T> a, DView<c
   load_f<V>(a.pix(pix) + c0, av);
   load_f<V>(bv.pix(pix) + c0, b2);
 #pragma unroll
-  for (int q = 0; q < V; ++q) o[q] = av[q] + gate * b2[q];
+  for (int q = 0; q < V; ++q) o[q] = __builtin_fmaf(gate, b2[q], av[q]);
   store_f<V>(y.pix(pix) + c0, o);
 }
 
@@ -421,18 +421,14 @@ __global__ __launch_bounds__(256) void dysample_kernel(DView<const T> x, DView<c
   float acc[V];
 #pragma unroll
   for (int q = 0; q < V; ++q) {
-    acc[q] = 0.f;
-    acc[q] += vnw[q] * wnw;
-    acc[q] += vne[q] * kne;
-    acc[q] += vsw[q] * ksw;
-    acc[q] += vse[q] * kse;
+    acc[q] = blend4(vnw[q], wnw, vne[q], kne, vsw[q], ksw, vse[q], kse);
   }
   store_f<V>(y.at(b, oy2, ox2) + c0, acc);
   if (y2.p) {  // fused FullPAD_Tunnel (block.py:1954-1956) on this output: y2 = a2 * T(y) + b2 * r2
     float rv[V], o2[V];
     load_f<V>(r2.at(b, oy2, ox2) + c0, rv);
 #pragma unroll
-    for (int q = 0; q < V; ++q) o2[q] = a2 * float(T(acc[q])) + b2 * rv[q];
+    for (int q = 0; q < V; ++q) o2[q] = pad_mix(a2, round_to<T>(acc[q]), b2, rv[q]);
     store_f<V>(y2.at(b, oy2, ox2) + c0, o2);
   }
 }

@@ -95,6 +95,11 @@ class DySampleDesc(C.Structure):
                 ("a2", C.c_float), ("b2", C.c_float)]
 
 
+class DySample2Desc(C.Structure):
+    _fields_ = [("x", View), ("off_w", C.c_void_p), ("off_b", C.c_void_p), ("groups", C.c_int32), ("y", View),
+                ("y2", View), ("r2", View), ("a2", C.c_float), ("b2", C.c_float)]
+
+
 class BottleneckDesc(C.Structure):
     _fields_ = [("x", View), ("y", View), ("c", C.c_int32), ("add", C.c_int32), ("tile_h", C.c_int32),
                 ("params", C.c_void_p), ("c_mid", C.c_int32), ("pw", C.c_int32)]
@@ -135,6 +140,7 @@ SIGNATURES = {
     "ydbl_hg_propagate": ([C.POINTER(HgDesc), _P], C.c_int),
     "ydbl_hg_fused_lds": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_hg_fused": ([C.POINTER(HgDesc), _P], C.c_int),
+    "ydbl_dysample2": ([C.POINTER(DySample2Desc), _P], C.c_int),
     "ydbl_detect_decode": ([C.POINTER(DecodeDesc), _P], C.c_int),
     "ydbl_pred_candidates": ([C.POINTER(PredCandDesc), _P], C.c_int),
     "ydbl_nms_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),

@@ -882,6 +882,16 @@ class DySample(nn.Module):
         # offset = 0.25 * conv1x1(x) + init_pos  ->  folded into the conv weights/bias (0.25 is exact)
         w = self.offset.weight.detach().float().cpu() * 0.25
         b = self.offset.bias.detach().float().cpu() * 0.25 + self.init_pos.detach().float().cpu().view(-1)
+        if not os.environ.get("YDBL_DS2_OFF") and self.groups == 4 and x.c in (64, 128, 256):
+            # offset conv + sample in one launch (csrc/dysample2.hip), bit-identical to the pair below
+            y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)
+            wd = plan.const(w.reshape(8 * self.groups, x.c).to(plan.dtype))
+            bd = plan.const(b)
+            d = _lib.DySample2Desc(x.struct(), wd.data_ptr(), bd.data_ptr(), self.groups, y.struct(), _null_view(),
+                                   _null_view(), 0.0, 0.0)
+            plan.launch("ydbl_dysample2", d, what="DySample.fused", keep=[d, wd, bd])
+            plan.note_writer(y, d)
+            return y
         off = plan.alloc(x.n, x.h, x.w, 8 * self.groups)
         emit_conv2d(plan, self.offset, x, off, w, b, what="DySample.offset")
         y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)

@@ -140,7 +140,7 @@ class Plan:
         for v in (y2, r2):
             if (v.n, v.h, v.w, v.c) != (y.n, y.h, y.w, y.c) or _lib.dtype_code(v.dtype) != y.dtype or v.cs % 4:
                 return None
-            if isinstance(d, _lib.DySampleDesc):
+            if isinstance(d, (_lib.DySampleDesc, _lib.DySample2Desc)):
                 vec = 16 // v.base.element_size()
                 if v.cs % vec or v.c % vec or v.ptr % 16:
                     return None
