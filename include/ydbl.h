@@ -40,6 +40,7 @@
  *   ydbl_dysample(_ex)     <- DySample.sample modules_upsample/DySample.py:48-61 (grid_sample border)
  *   ydbl_dysample2         <- DySample.forward DySample.py:63-81 (offset conv + sample, one launch)
  *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
+ *   ydbl_lsk_attn/_out     <- LSKblock.forward LSKA.py:43-52 (conv1 | conv2 + stats; gate + conv + x *)
  *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708 (ydbl_hg_fused: the whole
  *                             AdaHGConv incl. pre_head_proj block.py:1645, one launch)
  *   ydbl_detect_decode     <- Detect._inference head.py:143-181 + DFL block.py:79-83 +
@@ -221,6 +222,26 @@ int ydbl_dysample2(const ydbl_dysample2_desc* d, void* stream);
 int ydbl_lsk_gate(const ydbl_view* attn, const float* sw, const float* sb, const ydbl_view* out,
                   void* workspace, void* stream);
 int64_t ydbl_lsk_gate_workspace(int32_t n, int32_t h, int32_t w);
+/* LSKblock after its depthwise pair (LSKA.py:43-52) in two launches, fp16, dim in {256, 512}:
+ *   ydbl_lsk_attn: attn = [conv1(a1) + b1 | conv2(a2) + b2] (w12 rows 0..dim/2-1 = conv1, the rest conv2,
+ *                  each [dim/2][dim] K-contiguous fp16, b12 fp32 [dim]) and, per pixel, agg = [mean_c, max_c](attn)
+ *                  (fp32 [n*h*w][2] in `agg`, the rounded attn reduced in ydbl_lsk_gate's order);
+ *   ydbl_lsk_out:  y = x * (conv(a1' * sig0 + a2' * sig1) + b), sig = sigmoid(squeeze7x7(agg) + sb), w [dim][dim/2]
+ *                  fp16 K-contiguous, b fp32 [dim] -- the gate never leaves the CU.
+ * Bit-identical to ydbl_conv2d_nhwc (conv1, conv2) + ydbl_lsk_gate + ydbl_conv2d_nhwc (conv, RES_MUL) where
+ * those run the block GEMM (dim 256).  a1, a2, attn, x, y: [n,h,w,dim] views (channel stride multiple of 8). */
+typedef struct {
+  ydbl_view x, a1, a2, attn, y;
+  const void* w12;
+  const float* b12;
+  const float* sw;  /* conv_squeeze fp32 [2][2][7][7] */
+  const float* sb;  /* [2] */
+  const void* w;
+  const float* b;
+  float* agg;       /* ydbl_lsk_gate_workspace(n, h, w) bytes */
+} ydbl_lsk_desc;
+int ydbl_lsk_attn(const ydbl_lsk_desc* d, void* stream);
+int ydbl_lsk_out(const ydbl_lsk_desc* d, void* stream);
 
 /* Adaptive hypergraph (AdaHGConv), tokens = NHWC pixels of view x (D = x.c, N = h*w). */
 typedef struct {

@@ -47,6 +47,7 @@ STRUCTS = {
     "ydbl_dsbneck_desc": "DsBneckDesc",
     "ydbl_dysample_desc": "DySampleDesc",
     "ydbl_dysample2_desc": "DySample2Desc",
+    "ydbl_lsk_desc": "LskDesc",
 }
 
 

@@ -1152,3 +1152,40 @@ def test_dysample_fused_bit_identical(dtype, c, shape, spread, fullpad, monkeypa
     assert torch.equal(outs[0][0], outs[1][0]), (outs[0][0] - outs[1][0]).abs().max()
     if fullpad:
         assert torch.equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("c,shape,sliced", [(256, (16, 256, 20, 20), False), (256, (3, 256, 7, 11), True),
+                                            (512, (2, 512, 20, 20), False)])
+def test_lsk_fused_bit_identical(c, shape, sliced, monkeypatch):
+    """ydbl_lsk_attn + ydbl_lsk_out (conv1 | conv2 + stats, gate + conv + x* in two launches) == conv1, conv2,
+    ydbl_lsk_gate, conv (RES_MUL): bit for bit at dim 256, where the unfused 1x1s run the block GEMM (at 512 the
+    unfused conv1/conv2 take the wave-split-K kernel, another accumulation order: fp16 tolerance there)."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+
+    torch.manual_seed(c + shape[2])
+    o = om.LSKblock(c).eval()
+    m = M.LSKblock(c)
+    m.load_state_dict(o.state_dict())
+    x = torch.randn(*shape)
+    outs = []
+    for fused in ("1", ""):
+        if fused:
+            monkeypatch.delenv("YDBL_LSK_UNFUSED", raising=False)
+        else:
+            monkeypatch.setenv("YDBL_LSK_UNFUSED", "1")
+        plan = _plan(torch.float16)
+        xv = _tv_from_nchw(plan, x)
+        out = plan.alloc(shape[0], shape[2], shape[3], c + 16).cslice(8, c) if sliced else None
+        y = m.emit(plan, xv, out)
+        whats = [st.what for st in plan.steps]
+        assert ("LSK.gate+conv" in whats) == bool(fused), whats
+        _run(plan)
+        outs.append(y.nchw().float().cpu())
+    if c == 256:
+        assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+    else:
+        torch.testing.assert_close(outs[0], outs[1], rtol=2e-3, atol=2e-3)
+    with torch.no_grad():
+        ref = o(x)
+    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)

@@ -137,6 +137,12 @@ __device__ __forceinline__ float pad_mix(float a2, float y, float b2, float r) {
   if (a2 == 1.0f) return __builtin_fmaf(b2, r, y);
   return __builtin_fmaf(a2, y, b2 * r);
 }
+// LSKblock gate attn1 * s0 + attn2 * s1 (LSKA.py:50): the first product rounded, the second fused
+__device__ __forceinline__ float gate_mix(float a1, float s0, float a2, float s1) {
+  float o = a1 * s0;
+  asm volatile("" : "+v"(o));
+  return __builtin_fmaf(a2, s1, o);
+}
 // bilinear blend in grid_sample's nw, ne, sw, se order, one rounding per term
 __device__ __forceinline__ float blend4(float vnw, float wnw, float vne, float wne, float vsw, float wsw, float vse,
                                         float wse) {

@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256) void lsk_gate_kernel(DView<const T> attn, cons
   load_f<V>(attn.pix(pix) + c0, a1);
   load_f<V>(attn.pix(pix) + half + c0, a2);
 #pragma unroll
-  for (int q = 0; q < V; ++q) o[q] = a1[q] * s0 + a2[q] * s1;
+  for (int q = 0; q < V; ++q) o[q] = gate_mix(a1[q], s0, a2[q], s1);
   store_f<V>(out.pix(pix) + c0, o);
 }
 

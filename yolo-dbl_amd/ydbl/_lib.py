@@ -100,6 +100,12 @@ class DySample2Desc(C.Structure):
                 ("y2", View), ("r2", View), ("a2", C.c_float), ("b2", C.c_float)]
 
 
+class LskDesc(C.Structure):
+    _fields_ = [("x", View), ("a1", View), ("a2", View), ("attn", View), ("y", View), ("w12", C.c_void_p),
+                ("b12", C.c_void_p), ("sw", C.c_void_p), ("sb", C.c_void_p), ("w", C.c_void_p), ("b", C.c_void_p),
+                ("agg", C.c_void_p)]
+
+
 class BottleneckDesc(C.Structure):
     _fields_ = [("x", View), ("y", View), ("c", C.c_int32), ("add", C.c_int32), ("tile_h", C.c_int32),
                 ("params", C.c_void_p), ("c_mid", C.c_int32), ("pw", C.c_int32)]
@@ -135,6 +141,8 @@ SIGNATURES = {
     "ydbl_dysample_ex": ([C.POINTER(DySampleDesc), _P], C.c_int),
     "ydbl_lsk_gate": ([_VP, _P, _P, _VP, _P, _P], C.c_int),
     "ydbl_lsk_gate_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_lsk_attn": ([C.POINTER(LskDesc), _P], C.c_int),
+    "ydbl_lsk_out": ([C.POINTER(LskDesc), _P], C.c_int),
     "ydbl_hg_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_hg_context": ([C.POINTER(HgDesc), _P], C.c_int),
     "ydbl_hg_propagate": ([C.POINTER(HgDesc), _P], C.c_int),

@@ -916,6 +916,26 @@ class LSKblock(nn.Module):
     def emit(self, plan, x, out=None):
         half = self.conv1.out_channels
         a1, a2 = emit_dw_pair(plan, self.conv0, self.conv_spatial, x, what="LSK.dw5+dw7d3")
+        y = out if out is not None else plan.alloc(x.n, x.h, x.w, x.c)
+        if (plan.dtype == torch.float16 and x.c in (256, 512) and not os.environ.get("YDBL_LSK_UNFUSED")
+                and x.cs % 8 == 0 and y.cs % 8 == 0 and y.base is not x.base):
+            # conv1 | conv2 + stats, then gate + conv + x * in two launches (csrc/lsk.hip)
+            attn = plan.alloc(x.n, x.h, x.w, 2 * half)
+            ws = plan.scratch(_lib.lib.ydbl_lsk_gate_workspace(x.n, x.h, x.w))
+            c = plan.const
+            w12 = c(torch.cat([self.conv1.weight.detach().float().reshape(half, -1),
+                               self.conv2.weight.detach().float().reshape(half, -1)], 0).to(plan.dtype).contiguous())
+            b12 = c(torch.cat([self.conv1.bias.detach().float(), self.conv2.bias.detach().float()]))
+            sw, sb = c(self.conv_squeeze.weight.float()), c(self.conv_squeeze.bias.float())
+            wo = c(self.conv.weight.detach().float().reshape(x.c, half).to(plan.dtype).contiguous())
+            bo = c(self.conv.bias.detach().float())
+            d = _lib.LskDesc(x.struct(), a1.struct(), a2.struct(), attn.struct(), y.struct(), w12.data_ptr(),
+                             b12.data_ptr(), sw.data_ptr(), sb.data_ptr(), wo.data_ptr(), bo.data_ptr(), ws.data_ptr())
+            keep = [d, ws, w12, b12, sw, sb, wo, bo]
+            plan.launch("ydbl_lsk_attn", d, what="LSK.conv12+stats", keep=keep)
+            plan.launch("ydbl_lsk_out", d, what="LSK.gate+conv", keep=keep)
+            plan.note_writer(y, d)
+            return y
         attn = plan.alloc(x.n, x.h, x.w, 2 * half)
         emit_conv2d(plan, self.conv1, a1, attn.cslice(0, half), what="LSK.conv1")
         emit_conv2d(plan, self.conv2, a2, attn.cslice(half, half), what="LSK.conv2")
@@ -925,7 +945,7 @@ class LSKblock(nn.Module):
         sb = plan.const(self.conv_squeeze.bias.float())
         plan.launch("ydbl_lsk_gate", attn.struct(), sw.data_ptr(), sb.data_ptr(), gated.struct(), ws.data_ptr(),
                     what="LSK.gate", keep=[sw, sb, ws])
-        return emit_conv2d(plan, self.conv, gated, out, res=x, res_mode=_lib.RES_MUL, what="LSK.conv")
+        return emit_conv2d(plan, self.conv, gated, y, res=x, res_mode=_lib.RES_MUL, what="LSK.conv")
 
 
 # =============================================================================== head

@@ -134,7 +134,7 @@ class Plan:
         launch-time rules of that entry point: same shape and dtype as y, channel stride % 4 for the
         conv epilogue (ydbl_conv2d_nhwc), 16-byte vectors and pointers for ydbl_dysample_ex."""
         _, d = writer
-        if d.y2.ptr:
+        if not hasattr(d, "y2") or d.y2.ptr:  # e.g. ydbl_lsk_out: registered as a writer, no second output
             return None
         y = d.y
         for v in (y2, r2):
