@@ -88,14 +88,6 @@ def stem2_traffic(step, elsize):
     return d.n * d.cin * d.h * d.w * 4 + _px(d.y) * d.y.c * elsize, flops
 
 
-def dsbneck_traffic(step, elsize):
-    """ydbl_dsbottleneck_nhwc: x read (+ residual), y written; the intermediate stays on chip."""
-    d = step.args[0]
-    c = d.x.c
-    byts = (_px(d.x) * c * (2 if d.add else 1) + _px(d.y) * c) * elsize
-    return byts, 2.0 * _px(d.y) * c * (9 + c + 49 + c)
-
-
 def dysample_traffic(step, elsize):
     """ydbl_dysample_ex: x + offsets read, the 2x-upsampled y written (+ fused FullPAD second output)."""
     d = step.args[0]
@@ -168,7 +160,6 @@ def hg_fused_traffic(step, elsize):
 TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("dsconv", dsconv_traffic),
            "ydbl_dysample2": ("dysample", dysample2_traffic), "ydbl_hg_fused": ("hypergraph", hg_fused_traffic),
            "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
-           "ydbl_dsbottleneck_nhwc": ("dsbottleneck", dsbneck_traffic),
            "ydbl_dysample_ex": ("dysample", dysample_traffic)}
 
 

@@ -135,24 +135,6 @@ typedef struct {
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 
-/* DSBottleneck in one launch (U/nn/modules/block.py:1408-1444; replaces the two DSConv forwards of
- * :1436-1440 and the shortcut add): y = [x +] SiLU(pw2(dw7(t)) + b2), t = SiLU(pw1(dw3(x)) + b1),
- * DSConv(c, c, 3) -> DSConv(c, c, 7), e = 1.  t stays on the CU (recomputed on a 3-pixel halo per
- * 8x8 tile); bit-identical to two ydbl_dsconv_nhwc launches.  fp16 views, C = 64, y must not alias x.
- * dw*_w fp32 [k*k][C] (tap-major), pw*_w fp16 [C][kpad] (BN folded, kpad = C), b* fp32 [C]. */
-typedef struct {
-  ydbl_view x, y;
-  const float* dw1_w;
-  const void* pw1_w;
-  const float* b1;
-  const float* dw2_w;
-  const void* pw2_w;
-  const float* b2;
-  int32_t kpad;
-  int32_t add;
-} ydbl_dsbneck_desc;
-int ydbl_dsbottleneck_nhwc(const ydbl_dsbneck_desc* d, void* stream);
-
 /* Depthwise convolution (groups = C), fp32 arithmetic.
  * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).
  * w: fp32 [kh][kw][c]; bias: fp32 [c] or NULL; r: view or ignored. */

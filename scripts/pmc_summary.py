@@ -26,7 +26,6 @@ FAMILIES = {  # family -> (kernel-name keys, FETCH_SIZE multiplier)
     "conv2d": (("conv_igemm_kernel", "conv3x3_tile_kernel", "conv_wsk_kernel", "conv3x3_halo_kernel",
                 "conv3x3_vw_kernel"), 2),
     "dsconv": (("dsconv_kernel",), 2),
-    "dsbottleneck": (("dsbneck_kernel",), 2),
     "bottleneck": (("bneck_kernel",), 2),
     "stem2": (("stem2_kernel",), 2),
     "stem": (("stem_kernel",), 2),

@@ -44,7 +44,6 @@ STRUCTS = {
     "ydbl_letterbox_desc": "LetterboxDesc",
     "ydbl_stem2_desc": "Stem2Desc",
     "ydbl_bottleneck_desc": "BottleneckDesc",
-    "ydbl_dsbneck_desc": "DsBneckDesc",
     "ydbl_dysample_desc": "DySampleDesc",
     "ydbl_dysample2_desc": "DySample2Desc",
     "ydbl_lsk_desc": "LskDesc",

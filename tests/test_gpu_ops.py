@@ -523,7 +523,9 @@ def test_stem(dtype, cout, s, h, w):
 
 
 @pytest.mark.parametrize("c0,n,h,w", [(8, 2, 64, 64), (16, 2, 37, 53), (8, 1, 640, 640), (16, 3, 17, 100),
-                                       (8, 2, 3, 5), (16, 1, 256, 320)])
+                                       (8, 2, 3, 5), (16, 1, 256, 320),
+                                       # > 1024 tiles: the persistent walk with next-tile prefetch (V4 and scalar loads)
+                                       (8, 4, 640, 640), (16, 4, 480, 640), (8, 3, 642, 638)])
 def test_stem2(c0, n, h, w):
     """ydbl_conv_stem2 (preprocess + Conv s1 + Conv s2, fp16) vs the two convs in fp32 on fp16-rounded
     operands, the intermediate rounded to fp16 as the unfused path stores it."""
@@ -780,47 +782,6 @@ def test_dsconv_fused(dtype, cin, cout, k, s, shape):
     plan = _plan(dtype)
     assert M.fused_dsconv_ok(p_mod.dw, _tv_from_nchw(plan, x), dtype)
     _module_parity(o, p_mod, [x], dtype, tol)
-
-
-@pytest.mark.parametrize("n,h,w,add,sliced", [(32, 40, 40, True, True), (3, 13, 21, True, False), (1, 8, 8, False, False),
-                                              (2, 5, 3, True, True), (2, 20, 20, False, True)])
-def test_dsbottleneck_fused(n, h, w, add, sliced):
-    """ydbl_dsbottleneck_nhwc (cv1 -> cv2 of DSBottleneck with t on the CU, U/nn/modules/block.py:1408-1444)
-    == the two ydbl_dsconv_nhwc launches it replaces, bit for bit, and close to the oracle (fp16)."""
-    import os
-
-    from oracle import model as om
-    from ydbl.nn import modules as M
-    from ydbl.utils.synthetic import trained_like_
-
-    torch.manual_seed(n * 100 + h)
-    o = trained_like_(om.DSBottleneck(64, 64, shortcut=add, e=1.0, k1=3, k2=7), seed=h).eval()
-    x = torch.randn(n, 64, h, w)
-    outs = []
-    for fused in (True, False):
-        pm = M.DSBottleneck(64, 64, shortcut=add, e=1.0, k1=3, k2=7)
-        pm.load_state_dict(o.state_dict())
-        plan = _plan(torch.float16)
-        xv = _tv_from_nchw(plan, x, cs_extra=8 if sliced else 0, c_off=8 if sliced else 0)
-        ybuf = plan.alloc(n, h, w, 64 + (16 if sliced else 0))
-        yv = ybuf.cslice(8, 64) if sliced else ybuf
-        if fused:
-            os.environ["YDBL_DSBNECK"] = "1"
-        try:
-            pm.emit(plan, xv, yv)
-        finally:
-            os.environ.pop("YDBL_DSBNECK", None)
-        kinds = [st.fn.__name__ for st in plan.steps]
-        assert kinds == (["ydbl_dsbottleneck_nhwc"] if fused else ["ydbl_dsconv_nhwc"] * 2), kinds
-        _run(plan)
-        outs.append(yv.nchw().float().cpu())
-    with torch.no_grad():
-        ref = o(x)
-    d = (outs[0] - outs[1]).abs()
-    print(f"fused vs two launches: max {d.max().item():.3g}, {int((d > 0).sum())} of {d.numel()} differ; "
-          f"vs oracle: fused {(outs[0] - ref).abs().max().item():.3g}, two {(outs[1] - ref).abs().max().item():.3g}")
-    assert torch.equal(outs[0], outs[1])
-    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])

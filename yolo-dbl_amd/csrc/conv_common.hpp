@@ -212,10 +212,44 @@ __device__ __forceinline__ void conv_tail_1x1(const ConvArgs<T>& p, const f32x4 
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float u = float(T(apply_act<T>(acc[i][j][q] + bv[i][q], p.act)));
+        const float u = round_to<T>(apply_act<T>(acc[i][j][q] + bv[i][q], p.act));  // y as stored
 #pragma unroll
         for (int k = 0; k < 4; ++k) part[k] = fmaf(u, wv[i][q][k], part[k]);
       }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      part[k] += __shfl_xor(part[k], 16);
+      part[k] += __shfl_xor(part[k], 32);
+    }
+    if (g == 0 && pv[j]) {
+      T* o = p.y3 + pp[j] * p.y3cs;
+      for (int k = 0; k < p.nt3; ++k) o[k] = T(part[k] + p.t3b[k]);
+    }
+  }
+}
+
+// The same tail from the values the epilogue stored (ys = y rounded to T, per lane [TN][TM][4]): no activation
+// recomputed.  Lanes of one pixel share pv, so the xor-shuffles only mix lanes of the same pixel.
+template <typename T, int TN, int TM>
+__device__ __forceinline__ void conv_tail_1x1_vals(const ConvArgs<T>& p, const float (&ys)[TN][TM][4],
+                                                   const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN],
+                                                   int g) {
+  float wv[TN][4][4];
+#pragma unroll
+  for (int i = 0; i < TN; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wv[i][q][k] = k < p.nt3 ? p.t3w[k * p.Cout + co[i] + q] : 0.f;
+#pragma unroll
+  for (int j = 0; j < TM; ++j) {
+    float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) part[k] = fmaf(ys[i][j][q], wv[i][q][k], part[k]);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       part[k] += __shfl_xor(part[k], 16);

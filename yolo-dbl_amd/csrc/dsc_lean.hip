@@ -25,7 +25,7 @@ namespace ydbl {
 
 __device__ __forceinline__ int lean_bswz(int row, int kv) { return row * 4 + (kv ^ (((row >> 2) & 1) << 1)); }
 
-template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false>
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false, bool TAIL = false>
 __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, const float* __restrict__ dww,
                                                           const float* __restrict__ dwb, int dw_act, int tiles_x,
                                                           int tiles_y, int ntiles) {
@@ -67,25 +67,43 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  int bid = xcd_remap(blockIdx.x, ntiles);
-  const int tx = bid % tiles_x;
-  bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const int iy0 = oy0 * S - p.PAD, ix0 = ox0 * S - p.PAD;
-
-  // ---- 1. one round trip: halo + taps (-> LDS), then A fragments + residual (-> VGPRs)
-  h8 xr[HIT];
+  const int cg = wave % NCG, wp = wave / NCG;
+  int co[TN];
 #pragma unroll
-  for (int it = 0; it < HIT; ++it) {
-    const int i = min(tid + it * NT, HV - 1);
-    const int cv = i % CV, px = i / CV;
-    const int hy = px / IW, hx = px - hy * IW;
-    const int iy = iy0 + hy, ix = ix0 + hx;
-    const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-    xr[it] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + cv * 8, p.x, ok);
-  }
+  for (int i = 0; i < TN; ++i) co[i] = (cg * TN + i) * 16 + 4 * g;  // this lane's 4 epilogue channels
+
+  struct Tile {
+    int b, oy0, ox0, iy0, ix0;
+  };
+  auto tile_of = [&](int t) {
+    int bid = xcd_remap(t, ntiles);
+    const int tx = bid % tiles_x;
+    bid /= tiles_x;
+    const int ty = bid % tiles_y;
+    Tile tl;
+    tl.b = bid / tiles_y;
+    tl.oy0 = ty * TH;
+    tl.ox0 = tx * TW;
+    tl.iy0 = tl.oy0 * S - p.PAD;
+    tl.ix0 = tl.ox0 * S - p.PAD;
+    return tl;
+  };
+  h8 xr[HIT];
+  auto load_halo = [&](const Tile& tl) {
+#pragma unroll
+    for (int it = 0; it < HIT; ++it) {
+      const int i = min(tid + it * NT, HV - 1);
+      const int cv = i % CV, px = i / CV;
+      const int hy = px / IW, hx = px - hy * IW;
+      const int iy = tl.iy0 + hy, ix = tl.ix0 + hx;
+      const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      xr[it] = vload_sel(p.x + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.xcs + cv * 8, p.x, ok);
+    }
+  };
+
+  // ---- 1. one round trip: halo + taps (-> LDS), then A fragments (+ residual, second GEMM input) (-> VGPRs)
+  const Tile tl = tile_of(blockIdx.x);
+  load_halo(tl);
   f32x4 wr[TIT];
 #pragma unroll
   for (int it = 0; it < TIT; ++it) {
@@ -94,32 +112,6 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[it][e] = float(T(w[e]));  // the reference's .half() weights
   }
-  const int cg = wave % NCG, wp = wave / NCG;
-  int co[TN];
-#pragma unroll
-  for (int i = 0; i < TN; ++i) co[i] = (cg * TN + i) * 16 + 4 * g;  // this lane's 4 epilogue channels
-  int64_t pp[TM];
-  bool pv[TM];
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    const int pt = wp + WPG * j;
-    const int op = pt * 16 + r16;
-    const int oy = oy0 + op / TW, ox = ox0 + op % TW;
-    pv[j] = pt < NTP && oy < p.Ho && ox < p.Wo;
-    pp[j] = pv[j] ? ((int64_t)b * p.Ho + oy) * p.Wo + ox : 0;
-  }
-#pragma unroll
-  for (int it = 0; it < HIT; ++it) {
-    const int i = tid + it * NT;
-    if (i < HV) {
-      const int cv = i % CV, px = i / CV;
-      const int hy = px / IW, hx = px - hy * IW;
-      *reinterpret_cast<h8*>(&s_x[(hy * IWP + hx) * NQ + cv * 2]) = xr[it];
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < TIT; ++it)
-    if (tid + it * NT < TAPV) s_w[tid + it * NT] = wr[it];
   h8 af[TN][NKS];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
@@ -127,156 +119,118 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
 #pragma unroll
     for (int m = 0; m < NKS; ++m) af[i][m] = vload(p.w + (int64_t)row * p.KPAD + m * 32 + g * 8);
   }
-  h8 x2r[X2IT];  // TG: the second GEMM input's tile (C3's cv2 branch), [pixel][8-channel vector]
-  if constexpr (TG) {
 #pragma unroll
-    for (int it = 0; it < X2IT; ++it) {
-      const int i = min(tid + it * NT, X2V - 1);
-      const int px = i / (CO / 8), cv = i % (CO / 8);
-      const int oy = oy0 + px / TW, ox = ox0 + px % TW;
-      const bool ok = oy < p.Ho && ox < p.Wo;
-      x2r[it] = vload_sel(p.g2x + (((int64_t)b * p.Ho + oy) * p.Wo + ox) * p.g2xcs + cv * 8, p.g2x, ok);
-    }
-  }
-  h4 rv[TN][TM];
-  if (p.res != YDBL_RES_NONE) {
-#pragma unroll
-    for (int j = 0; j < TM; ++j)
-#pragma unroll
-      for (int i = 0; i < TN; ++i) rv[i][j] = *reinterpret_cast<const h4*>(p.r + pp[j] * p.rcs + co[i]);
-  }
-  __syncthreads();
+  for (int it = 0; it < TIT; ++it)
+    if (tid + it * NT < TAPV) s_w[tid + it * NT] = wr[it];
 
-  // ---- 2. depthwise: task = (quad q, output row r, segment sg), quad fastest
   {
-    const int q = tid % NQ;
-    const int r = (tid / NQ) % TH;
-    const int sg = tid / (NQ * TH);
-    float a[CSEG][4];
-#pragma unroll
-    for (int c = 0; c < CSEG; ++c)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) a[c][e] = 0.f;
-    constexpr int KU = K <= 3 ? K : 1;  // the 7x7: one input row's window + taps live at a time
-#pragma unroll KU
-    for (int ky = 0; ky < K; ++ky) {
-      const h4* xrow = &s_x[((r * S + ky) * IWP + sg * CSEG * S) * NQ + q];
-      float xs[SEGW][4];
-#pragma unroll
-      for (int i = 0; i < SEGW; ++i) {
-        const h4 v = xrow[i * NQ];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) xs[i][e] = float(v[e]);
-      }
-      f32x4 wv[K];
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) wv[kx] = s_w[(ky * K + kx) * NQ + q];
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx)
-#pragma unroll
-        for (int c = 0; c < CSEG; ++c)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) a[c][e] = fmaf(xs[c * S + kx][e], wv[kx][e], a[c][e]);
-    }
-    if (dwb) {  // uniform: DWConv (+ folded BN) bias and activation before the pointwise
-      const f32x4 bq = *reinterpret_cast<const f32x4*>(dwb + q * 4);
-#pragma unroll
-      for (int c = 0; c < CSEG; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) a[c][e] = apply_act<T>(a[c][e] + bq[e], dw_act);
-    }
-    const int ks = q / 8, ql = q % 8;  // k-step and 4-channel slot of this quad
-#pragma unroll
-    for (int c = 0; c < CSEG; ++c) {
-      const int px = r * TW + sg * CSEG + c;
-      *(reinterpret_cast<h4*>(&s_b[ks * NPX * 4 + lean_bswz(px, ql >> 1)]) + (ql & 1)) = to_h4_rne(a[c]);
-    }
-  }
-  __syncthreads();
-
-  // ---- 3. pointwise MFMA over all k-steps, epilogue
-  f32x4 acc[TN][TM];
-#pragma unroll
-  for (int i = 0; i < TN; ++i)
-#pragma unroll
-    for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int m = 0; m < NKS; ++m)
+    int64_t pp[TM];
+    bool pv[TM];
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       const int pt = wp + WPG * j;
-      if (TM * WPG == NTP || pt < NTP) {
-        const h8 bf = s_b[m * NPX * 4 + lean_bswz(pt * 16 + r16, g)];
-#pragma unroll
-        for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][m], bf, acc[i][j], 0, 0, 0);
-      }
+      const int op = pt * 16 + r16;
+      const int oy = tl.oy0 + op / TW, ox = tl.ox0 + op % TW;
+      pv[j] = pt < NTP && oy < p.Ho && ox < p.Wo;
+      pp[j] = pv[j] ? ((int64_t)tl.b * p.Ho + oy) * p.Wo + ox : 0;
     }
-  float bv[TN][4];
+    h8 x2r[X2IT];  // TG: the second GEMM input's tile (C3's cv2 branch), [pixel][8-channel vector]
+    if constexpr (TG) {
 #pragma unroll
-  for (int i = 0; i < TN; ++i) load_f<4>(p.bias + co[i], bv[i]);
-#pragma unroll
-  for (int j = 0; j < TM; ++j) {
-    if (!pv[j]) continue;
-#pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      float v[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] + bv[i][q], p.act);
-      if (p.res == YDBL_RES_ADD) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) + v[q];
-      } else if (p.res == YDBL_RES_MUL) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) * v[q];
-      }
-      if constexpr (TG) {  // y (rounded as the unfused path stores it) -> the trailing GEMM's B tile
-        const int px = (wp + WPG * j) * 16 + r16, c = co[i];
-        *(reinterpret_cast<h4*>(&s_g[(c >> 5) * NPX * 4 + lean_bswz(px, (c >> 3) & 3)]) + ((c >> 2) & 1)) =
-            to_h4_rne(v);
-      } else {
-        store_f<4>(p.y + pp[j] * p.ycs + co[i], v);
-      }
-    }
-  }
-  if constexpr (NCG == 1 && TN == 4 && !TG) {  // Detect class conv over the 64 output channels (host-checked CO == 64)
-    if (p.t3w) conv_tail_1x1<T, TN, TM>(p, acc, pp, pv, co, g);
-  }
-  if constexpr (TG) {
-    // ---- 4. trailing GEMM: g2y = act(W2 [y ; g2x] + b2), K = 2*CO in channel order (the unfused cv3's k-steps)
-#pragma unroll
-    for (int it = 0; it < X2IT; ++it) {
-      const int i = tid + it * NT;
-      if (i < X2V) {
+      for (int it = 0; it < X2IT; ++it) {
+        const int i = min(tid + it * NT, X2V - 1);
         const int px = i / (CO / 8), cv = i % (CO / 8);
-        s_g[(CO / 32 + cv / 4) * NPX * 4 + lean_bswz(px, cv & 3)] = x2r[it];
+        const int oy = tl.oy0 + px / TW, ox = tl.ox0 + px % TW;
+        const bool ok = oy < p.Ho && ox < p.Wo;
+        x2r[it] = vload_sel(p.g2x + (((int64_t)tl.b * p.Ho + oy) * p.Wo + ox) * p.g2xcs + cv * 8, p.g2x, ok);
       }
     }
-    h8 a2[TN][NKS2];
+    h4 rv[TN][TM];
+    if (p.res != YDBL_RES_NONE) {
 #pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int row = (cg * TN + i) * 16 + r16;
+      for (int j = 0; j < TM; ++j)
 #pragma unroll
-      for (int m = 0; m < NKS2; ++m) a2[i][m] = vload(p.g2w + (int64_t)row * (2 * CO) + m * 32 + g * 8);
+        for (int i = 0; i < TN; ++i) rv[i][j] = *reinterpret_cast<const h4*>(p.r + pp[j] * p.rcs + co[i]);
     }
-    float b2v[TN][4];
 #pragma unroll
-    for (int i = 0; i < TN; ++i) load_f<4>(p.g2b + co[i], b2v[i]);
+    for (int it = 0; it < HIT; ++it) {
+      const int i = tid + it * NT;
+      if (i < HV) {
+        const int cv = i % CV, px = i / CV;
+        const int hy = px / IW, hx = px - hy * IW;
+        *reinterpret_cast<h8*>(&s_x[(hy * IWP + hx) * NQ + cv * 2]) = xr[it];
+      }
+    }
     __syncthreads();
+
+    // ---- 2. depthwise: task = (quad q, output row r, segment sg), quad fastest
+    {
+      const int q = tid % NQ;
+      const int r = (tid / NQ) % TH;
+      const int sg = tid / (NQ * TH);
+      float a[CSEG][4];
+#pragma unroll
+      for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[c][e] = 0.f;
+      constexpr int KU = K <= 3 ? K : 1;  // the 7x7: one input row's window + taps live at a time
+#pragma unroll KU
+      for (int ky = 0; ky < K; ++ky) {
+        const h4* xrow = &s_x[((r * S + ky) * IWP + sg * CSEG * S) * NQ + q];
+        float xs[SEGW][4];
+#pragma unroll
+        for (int i = 0; i < SEGW; ++i) {
+          const h4 v = xrow[i * NQ];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) xs[i][e] = float(v[e]);
+        }
+        f32x4 wv[K];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) wv[kx] = s_w[(ky * K + kx) * NQ + q];
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+          for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) a[c][e] = fmaf(xs[c * S + kx][e], wv[kx][e], a[c][e]);
+      }
+      if (dwb) {  // uniform: DWConv (+ folded BN) bias and activation before the pointwise
+        const f32x4 bq = *reinterpret_cast<const f32x4*>(dwb + q * 4);
+#pragma unroll
+        for (int c = 0; c < CSEG; ++c)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[c][e] = apply_act<T>(a[c][e] + bq[e], dw_act);
+      }
+      const int ks = q / 8, ql = q % 8;  // k-step and 4-channel slot of this quad
+#pragma unroll
+      for (int c = 0; c < CSEG; ++c) {
+        const int px = r * TW + sg * CSEG + c;
+        *(reinterpret_cast<h4*>(&s_b[ks * NPX * 4 + lean_bswz(px, ql >> 1)]) + (ql & 1)) = to_h4_rne(a[c]);
+      }
+    }
+    __syncthreads();
+
+    // ---- 3. pointwise MFMA over all k-steps, epilogue
+    f32x4 acc[TN][TM];
 #pragma unroll
     for (int i = 0; i < TN; ++i)
 #pragma unroll
       for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int m = 0; m < NKS2; ++m)
+    for (int m = 0; m < NKS; ++m)
 #pragma unroll
       for (int j = 0; j < TM; ++j) {
         const int pt = wp + WPG * j;
         if (TM * WPG == NTP || pt < NTP) {
-          const h8 bf = s_g[m * NPX * 4 + lean_bswz(pt * 16 + r16, g)];
+          const h8 bf = s_b[m * NPX * 4 + lean_bswz(pt * 16 + r16, g)];
 #pragma unroll
-          for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i][m], bf, acc[i][j], 0, 0, 0);
+          for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][m], bf, acc[i][j], 0, 0, 0);
         }
       }
+    float bv[TN][4];
+#pragma unroll
+    for (int i = 0; i < TN; ++i) load_f<4>(p.bias + co[i], bv[i]);
+    float ys[TAIL ? TN : 1][TAIL ? TM : 1][4];  // TAIL: the stored y values for the class conv
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
       if (!pv[j]) continue;
@@ -284,19 +238,99 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
       for (int i = 0; i < TN; ++i) {
         float v[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] + b2v[i][q], p.g2act);
-        store_f<4>(p.g2y + pp[j] * p.g2ycs + co[i], v);
+        for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] + bv[i][q], p.act);
+        if (p.res == YDBL_RES_ADD) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) + v[q];
+        } else if (p.res == YDBL_RES_MUL) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = float(rv[i][j][q]) * v[q];
+        }
+        if constexpr (TG) {  // y (rounded as the unfused path stores it) -> the trailing GEMM's B tile
+          const int px = (wp + WPG * j) * 16 + r16, c = co[i];
+          *(reinterpret_cast<h4*>(&s_g[(c >> 5) * NPX * 4 + lean_bswz(px, (c >> 3) & 3)]) + ((c >> 2) & 1)) =
+              to_h4_rne(v);
+        } else {
+          store_f<4>(p.y + pp[j] * p.ycs + co[i], v);
+          if constexpr (TAIL) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ys[i][j][q] = round_to<T>(v[q]);
+          }
+        }
+      }
+    }
+    if constexpr (TAIL && NCG == 1 && TN == 4 && !TG) {  // Detect class conv over the 64 output channels (CO == 64)
+      conv_tail_1x1_vals<T, TN, TM>(p, ys, pp, pv, co, g);
+    }
+    if constexpr (TG) {
+      // ---- 4. trailing GEMM: g2y = act(W2 [y ; g2x] + b2), K = 2*CO in channel order (the unfused cv3's k-steps)
+#pragma unroll
+      for (int it = 0; it < X2IT; ++it) {
+        const int i = tid + it * NT;
+        if (i < X2V) {
+          const int px = i / (CO / 8), cv = i % (CO / 8);
+          s_g[(CO / 32 + cv / 4) * NPX * 4 + lean_bswz(px, cv & 3)] = x2r[it];
+        }
+      }
+      h8 a2[TN][NKS2];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) {
+        const int row = (cg * TN + i) * 16 + r16;
+#pragma unroll
+        for (int m = 0; m < NKS2; ++m) a2[i][m] = vload(p.g2w + (int64_t)row * (2 * CO) + m * 32 + g * 8);
+      }
+      float b2v[TN][4];
+#pragma unroll
+      for (int i = 0; i < TN; ++i) load_f<4>(p.g2b + co[i], b2v[i]);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < TN; ++i)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < NKS2; ++m)
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int pt = wp + WPG * j;
+          if (TM * WPG == NTP || pt < NTP) {
+            const h8 bf = s_g[m * NPX * 4 + lean_bswz(pt * 16 + r16, g)];
+#pragma unroll
+            for (int i = 0; i < TN; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a2[i][m], bf, acc[i][j], 0, 0, 0);
+          }
+        }
+#pragma unroll
+      for (int j = 0; j < TM; ++j) {
+        if (!pv[j]) continue;
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(acc[i][j][q] + b2v[i][q], p.g2act);
+          store_f<4>(p.g2y + pp[j] * p.g2ycs + co[i], v);
+        }
       }
     }
   }
 }
 
-template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false>
-static void lean_go(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool TAIL>
+static void lean_go2(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
   const int ntiles = a.N * tiles_y * tiles_x;
-  dsc_lean_kernel<C, CO, K, S, TH, TW, NT, TG><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y,
-                                                                               ntiles);
+  // (measured and not kept: a persistent walk with the next tile's halo prefetched -- 2-3 workgroups per CU,
+  // VGPR-bound, slower or even on every DBL-n shape but the 80^2 stride-2 one, which the chunked kernel takes)
+  dsc_lean_kernel<C, CO, K, S, TH, TW, NT, TG, TAIL><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x,
+                                                                                     tiles_y, ntiles);
+}
+
+// the Detect class-conv tail (p.t3w, CO 64 only) as its own instance: its 64 tail weights per lane would
+// otherwise set the register budget of every launch of the shape
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false>
+static void lean_go(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
+  if constexpr (CO == 64 && !TG) {
+    if (a.t3w) return lean_go2<C, CO, K, S, TH, TW, NT, TG, true>(a, dww, dwb, dw_act, s);
+  }
+  lean_go2<C, CO, K, S, TH, TW, NT, TG, false>(a, dww, dwb, dw_act, s);
 }
 
 // Shapes built (DBL-n / DBL-s neck and head, fp16): DSBottleneck's k3 / k7 DSConvs at 64 / 128 channels, the
@@ -317,14 +351,16 @@ bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dw
   if (st == 1 && k == 3) {
     if (c == 64 && co == 64) return lean_go<64, 64, 3, 1, 8, 8, 256>(a, dww, dwb, dw_act, s), true;
     if (c == 128 && co == 128) return lean_go<128, 128, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
-    if (c == 128 && co == 64) return lean_go<128, 64, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
+    // 128 -> 64 (Detect P4 pair): the chunked kernel is faster (bs16 @40^2: 12.0 vs 17.4 us, scripts/kbench.py)
     if (c == 256 && co == 64) return lean_go<256, 64, 3, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
   }
   if (st == 1 && k == 7) {
     if (c == 64 && co == 64) return lean_go<64, 64, 7, 1, 8, 8, 256>(a, dww, dwb, dw_act, s), true;
     if (c == 128 && co == 128) return lean_go<128, 128, 7, 1, 8, 8, 512>(a, dww, dwb, dw_act, s), true;
   }
-  if (st == 2 && k == 3 && c == 128) {
+  // stride 2: the lean tile only below 12800 output pixels (bs16 80^2 -> 40^2: chunked 17.4 vs lean 28.4 us;
+  // 40^2 -> 20^2: lean 13.4 vs chunked 17.9 us per bs16 graph)
+  if (st == 2 && k == 3 && c == 128 && a.P <= 12800) {
     if (co == 128) return lean_go<128, 128, 3, 2, 4, 8, 512>(a, dww, dwb, dw_act, s), true;
     if (co == 256) return lean_go<128, 256, 3, 2, 4, 8, 512>(a, dww, dwb, dw_act, s), true;
   }

@@ -81,6 +81,9 @@ void stem2_pack(const float* w0, const float* b0, const float* w1, const float* 
   for (int i = 0; i < Cfg::C1; ++i) fb1[i] = b1[i];
 }
 
+// One workgroup per tile.  (Measured and not kept: a persistent walk over 2-8 tiles per CU with the next
+// tile's window prefetched during the current tile's convs -- 140-166 vs 136 us at bs32: the kernel is VALU-
+// issue-bound on the first conv's SiLU, not latency-bound.)
 template <int C0, int TW, int TH, bool V4>
 __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__ x, int H, int W, float scale,
                                                        const unsigned char* __restrict__ params,
@@ -93,66 +96,82 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   extern __shared__ __align__(16) unsigned char smem[];
   h4* in = reinterpret_cast<h4*>(smem);                        // [INH][INW] records
   unsigned char* l0 = smem + Cfg::IN_BYTES;                     // [CH][L0H][2][L0P] x 16 B
-
-  const int bid = xcd_remap(blockIdx.x, nblocks);
-  const int tx = bid % tiles_x;
-  const int ty = (bid / tiles_x) % tiles_y;
-  const int img = bid / (tiles_x * tiles_y);
-  const int oy0 = ty * TH, ox0 = tx * TW;
-  const int Y0 = 2 * oy0 - 1, X0 = 2 * ox0 - 1;                 // first-conv tile origin (image coords)
   const int64_t plane = (int64_t)H * W;
-  const float* xb = x + (int64_t)img * 3 * plane;
 
-  // ---- 1. input window, origin (Y0 - 1, X0 - 1); the slack past it is zeroed (a block-diagonal
+  struct Tile {
+    int img, oy0, ox0, Y0, X0;
+  };
+  auto tile_of = [&](int t) {
+    const int bid = xcd_remap(t, nblocks);
+    const int tx = bid % tiles_x;
+    const int ty = (bid / tiles_x) % tiles_y;
+    Tile tl;
+    tl.img = bid / (tiles_x * tiles_y);
+    tl.oy0 = ty * TH;
+    tl.ox0 = tx * TW;
+    tl.Y0 = 2 * tl.oy0 - 1;  // first-conv tile origin (image coords)
+    tl.X0 = 2 * tl.ox0 - 1;
+    return tl;
+  };
+
+  // ---- 1. input window, origin (Y0 - 1, X0 - 1); the slack past it is zeroed once (a block-diagonal
   // MFMA multiplies the other set's records by 0, which must not meet a NaN)
   if (threadIdx.x < Cfg::IN_BYTES / 8 - Cfg::INH * Cfg::INW) in[Cfg::INH * Cfg::INW + threadIdx.x] = h4{0, 0, 0, 0};
-  if constexpr (V4) {
-    // tasks = (row, 16-byte column group): three float4 loads (one per plane) -> 4 records.
-    // Group k covers image columns A + 4k .. A + 4k + 3 = record columns 4k - 2 .. 4k + 1, with
-    // A = X0 - 3 a multiple of 4, so with W % 4 == 0 a group is wholly inside or outside the image.
-    constexpr int NG = (Cfg::INW + 5) / 4;
-    constexpr int TASKS = Cfg::INH * NG;
-    constexpr int IT = (TASKS + 255) / 256;
-    const int A = X0 - 3;
-    f32x4 v[IT][3];
+  // V4 tasks = (row, 16-byte column group): three float4 loads (one per plane) -> 4 records.
+  // Group k covers image columns A + 4k .. A + 4k + 3 = record columns 4k - 2 .. 4k + 1, with
+  // A = X0 - 3 a multiple of 4, so with W % 4 == 0 a group is wholly inside or outside the image.
+  constexpr int NG = (Cfg::INW + 5) / 4;
+  constexpr int TASKS = V4 ? Cfg::INH * NG : Cfg::INH * Cfg::INW;
+  constexpr int IT = (TASKS + 255) / 256;
+  f32x4 v[IT][3];
+  auto load_window = [&](const Tile& tl) {
+    const float* xb = x + (int64_t)tl.img * 3 * plane;
+    if constexpr (V4) {
+      const int A = tl.X0 - 3;
 #pragma unroll
-    for (int u = 0; u < IT; ++u) {
-      const int t = threadIdx.x + u * 256;
-      const int r = t / NG, k = t - r * NG;
-      const int iy = Y0 - 1 + r, ix = A + 4 * k;
-      const bool ok = t < TASKS && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      const int64_t o = ok ? (int64_t)iy * W + ix : 0;
+      for (int u = 0; u < IT; ++u) {
+        const int t = threadIdx.x + u * 256;
+        const int r = t / NG, k = t - r * NG;
+        const int iy = tl.Y0 - 1 + r, ix = A + 4 * k;
+        const bool ok = t < TASKS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
-        v[u][c] = ok ? *reinterpret_cast<const f32x4*>(xb + c * plane + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int c = 0; c < 3; ++c)
+          v[u][c] = ok ? *reinterpret_cast<const f32x4*>(xb + c * plane + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < IT; ++u) {
+        const int t = threadIdx.x + u * 256;
+        const int r = t / Cfg::INW, c = t - r * Cfg::INW;
+        const int iy = tl.Y0 - 1 + r, ix = tl.X0 - 1 + c;
+        const bool ok = t < TASKS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        const int64_t o = ok ? (int64_t)iy * W + ix : 0;
+#pragma unroll
+        for (int ch = 0; ch < 3; ++ch) v[u][ch][0] = ok ? xb[ch * plane + o] : 0.f;
+      }
     }
+  };
+  auto store_window = [&]() {
 #pragma unroll
     for (int u = 0; u < IT; ++u) {
       const int t = threadIdx.x + u * 256;
       if (t >= TASKS) continue;
-      const int r = t / NG, k = t - r * NG;
+      if constexpr (V4) {
+        const int r = t / NG, k = t - r * NG;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int col = 4 * k - 2 + e;
-        if (col < 0 || col >= Cfg::INW) continue;
-        in[r * Cfg::INW + col] = h4{f16_rne(v[u][0][e] * scale), f16_rne(v[u][1][e] * scale),
-                                    f16_rne(v[u][2][e] * scale), (_Float16)0.f};
+        for (int e = 0; e < 4; ++e) {
+          const int col = 4 * k - 2 + e;
+          if (col < 0 || col >= Cfg::INW) continue;
+          in[r * Cfg::INW + col] = h4{f16_rne(v[u][0][e] * scale), f16_rne(v[u][1][e] * scale),
+                                      f16_rne(v[u][2][e] * scale), (_Float16)0.f};
+        }
+      } else {
+        in[t] = h4{f16_rne(v[u][0][0] * scale), f16_rne(v[u][1][0] * scale), f16_rne(v[u][2][0] * scale),
+                   (_Float16)0.f};
       }
     }
-  } else {
-    for (int t = threadIdx.x; t < Cfg::INH * Cfg::INW; t += 256) {
-      const int r = t / Cfg::INW, c = t - r * Cfg::INW;
-      const int iy = Y0 - 1 + r, ix = X0 - 1 + c;
-      h4 rec = h4{0, 0, 0, 0};
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        const int64_t o = (int64_t)iy * W + ix;
-        rec[0] = f16_rne(xb[o] * scale);
-        rec[1] = f16_rne(xb[plane + o] * scale);
-        rec[2] = f16_rne(xb[2 * plane + o] * scale);
-      }
-      in[t] = rec;
-    }
-  }
+  };
 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int g = lane >> 4, r16 = lane & 15;
@@ -180,42 +199,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
 #pragma unroll
   for (int q = 0; q < 4; ++q) bias0[q] = b0[4 * g + q];
   const int my_set = (4 * g) / Cfg::C0M, cbase = (4 * g) % Cfg::C0M;  // rows of D this lane holds
-  // workgroups whose first-conv window lies inside the image skip the per-pixel padding test
-  const bool interior = Y0 >= 0 && X0 >= 0 && Y0 + Cfg::L0H <= H && X0 + Cfg::L0W <= W;
   unsigned char* l0w = l0 + ((cbase >> 3) * Cfg::L0H * 2 * Cfg::L0P) * 16 + (cbase & 7) * 2;
-  __syncthreads();
-
-  // ---- 2. first conv, 16 * PS pixels per MFMA group
-  constexpr int P0V = Cfg::L0H * Cfg::INW;
-  const unsigned char* inb = reinterpret_cast<const unsigned char*>(in);
-  for (int pt = wave; pt * 16 * PS < P0V; pt += 4) {
-    const int p0 = pt * 16 * PS + r16;
-    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int m = 0; m < KS0; ++m) {
-      const h4 lo = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][0]);
-      const h4 hi = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][1]);
-      const h8 bf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[m], bf, acc, 0, 0, 0);
-    }
-    const int p = p0 + my_set * 16;
-    const int lr = p / Cfg::INW, lc = p - lr * Cfg::INW;
-    if (p >= P0V || lc >= Cfg::L0W) continue;
-    bool inside = true;
-    if (!interior) {
-      const int iy = Y0 + lr, ix = X0 + lc;
-      inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
-    }
-    h4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float sv = silu_fast(acc[q] + bias0[q]);
-      v[q] = f16_rne(inside ? sv : 0.f);
-    }
-    const int rec = lr * 2 * Cfg::L0P + (lc & 1) * Cfg::L0P + (lc >> 1);
-    *reinterpret_cast<h4*>(l0w + rec * 16) = v;
-  }
-
   // second-conv weights: k = tap*C0 + c; lane g of k-step m holds k = 32m + 8g .. +7
   h8 a1[Cfg::NT1][Cfg::KS1];
   int roff[Cfg::KS1];  // LDS byte offset of this lane's 8-channel chunk relative to pixel (0, 0)
@@ -234,31 +218,71 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   for (int t = 0; t < Cfg::NT1; ++t)
 #pragma unroll
     for (int q = 0; q < 4; ++q) bias1[t][q] = b1[16 * t + 4 * g + q];
-  __syncthreads();
 
-  // ---- 3. second conv: TH rows x TW cols, 16-pixel row segments
-  constexpr int SEG = TW / 16;
-  for (int st = wave; st < TH * SEG; st += 4) {
-    const int j = st / SEG, i = (st - j * SEG) * 16 + r16;
-    const unsigned char* pbase = l0 + ((2 * j) * 2 * Cfg::L0P + i) * 16;
-    f32x4 acc[Cfg::NT1];
+  const Tile tl = tile_of(blockIdx.x);
+  load_window(tl);
+  {
+    store_window();
+    __syncthreads();
+    // workgroups whose first-conv window lies inside the image skip the per-pixel padding test
+    const bool interior = tl.Y0 >= 0 && tl.X0 >= 0 && tl.Y0 + Cfg::L0H <= H && tl.X0 + Cfg::L0W <= W;
+
+    // ---- 2. first conv, 16 * PS pixels per MFMA group
+    constexpr int P0V = Cfg::L0H * Cfg::INW;
+    const unsigned char* inb = reinterpret_cast<const unsigned char*>(in);
+    for (int pt = wave; pt * 16 * PS < P0V; pt += 4) {
+      const int p0 = pt * 16 * PS + r16;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < Cfg::NT1; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int m = 0; m < KS0; ++m) {
+        const h4 lo = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][0]);
+        const h4 hi = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][1]);
+        const h8 bf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[m], bf, acc, 0, 0, 0);
+      }
+      const int p = p0 + my_set * 16;
+      const int lr = p / Cfg::INW, lc = p - lr * Cfg::INW;
+      if (p >= P0V || lc >= Cfg::L0W) continue;
+      bool inside = true;
+      if (!interior) {
+        const int iy = tl.Y0 + lr, ix = tl.X0 + lc;
+        inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+      }
+      h4 hv;
 #pragma unroll
-    for (int m = 0; m < Cfg::KS1; ++m) {
-      const h8 bf = *reinterpret_cast<const h8*>(pbase + roff[m]);
-#pragma unroll
-      for (int t = 0; t < Cfg::NT1; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[t][m], bf, acc[t], 0, 0, 0);
+      for (int q = 0; q < 4; ++q) {
+        const float sv = silu_fast(acc[q] + bias0[q]);
+        hv[q] = f16_rne(inside ? sv : 0.f);
+      }
+      const int rec = lr * 2 * Cfg::L0P + (lc & 1) * Cfg::L0P + (lc >> 1);
+      *reinterpret_cast<h4*>(l0w + rec * 16) = hv;
     }
-    const int oy = oy0 + j, ox = ox0 + i;
-    if (oy >= y.h || ox >= y.w) continue;
-    _Float16* yp = y.at(img, oy, ox);
+    __syncthreads();
+
+    // ---- 3. second conv: TH rows x TW cols, 16-pixel row segments
+    constexpr int SEG = TW / 16;
+    for (int st = wave; st < TH * SEG; st += 4) {
+      const int j = st / SEG, i = (st - j * SEG) * 16 + r16;
+      const unsigned char* pbase = l0 + ((2 * j) * 2 * Cfg::L0P + i) * 16;
+      f32x4 acc[Cfg::NT1];
 #pragma unroll
-    for (int t = 0; t < Cfg::NT1; ++t) {
-      float v[4];
+      for (int q = 0; q < Cfg::NT1; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = silu_fast(acc[t][q] + bias1[t][q]);
-      store_f<4>(yp + 16 * t + 4 * g, v);
+      for (int m = 0; m < Cfg::KS1; ++m) {
+        const h8 bf = *reinterpret_cast<const h8*>(pbase + roff[m]);
+#pragma unroll
+        for (int q = 0; q < Cfg::NT1; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[q][m], bf, acc[q], 0, 0, 0);
+      }
+      const int oy = tl.oy0 + j, ox = tl.ox0 + i;
+      if (oy >= y.h || ox >= y.w) continue;
+      _Float16* yp = y.at(tl.img, oy, ox);
+#pragma unroll
+      for (int q = 0; q < Cfg::NT1; ++q) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = silu_fast(acc[q][e] + bias1[q][e]);
+        store_f<4>(yp + 16 * q + 4 * g, o);
+      }
     }
   }
 }
@@ -298,21 +322,20 @@ extern "C" int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream) {
     const int tiles_x = (wo + tw - 1) / tw, tiles_y = (ho + th - 1) / th;
     const int64_t nb = (int64_t)tiles_x * tiles_y * d->n;
     if (nb > 0x7fffffff) return fail(YDBL_EINVAL, "stem2: grid too large");
-    kern<<<(unsigned)nb, 256, lds, s>>>(d->x, d->h, d->w, d->scale,
-                                        reinterpret_cast<const unsigned char*>(d->params), dview<_Float16>(d->y),
-                                        tiles_x, tiles_y, (int)nb);
+    kern<<<(unsigned)nb, 256, lds, s>>>(d->x, d->h, d->w, d->scale, reinterpret_cast<const unsigned char*>(d->params),
+                                        dview<_Float16>(d->y), tiles_x, tiles_y, (int)nb);
     return check_launch("ydbl_conv_stem2");
   };
   const bool v4 = d->w % 4 == 0 && (reinterpret_cast<uintptr_t>(d->x) & 15) == 0;
-  const char* ev = getenv("YDBL_STEM2_TH");  // A/B knob (read per launch): 4-row tiles
-  if (c0 == 8 && ev && atoi(ev) == 4)
-    return v4 ? go(stem2_kernel<8, 32, 4, true>, 32, 4, Stem2Cfg<8, 32, 4>::LDS)
-              : go(stem2_kernel<8, 32, 4, false>, 32, 4, Stem2Cfg<8, 32, 4>::LDS);
-  if (c0 == 8)
-    return v4 ? go(stem2_kernel<8, 32, 8, true>, 32, 8, Stem2Cfg<8, 32, 8>::LDS)
-              : go(stem2_kernel<8, 32, 8, false>, 32, 8, Stem2Cfg<8, 32, 8>::LDS);
-  if (c0 == 16)
-    return v4 ? go(stem2_kernel<16, 32, 8, true>, 32, 8, Stem2Cfg<16, 32, 8>::LDS)
-              : go(stem2_kernel<16, 32, 8, false>, 32, 8, Stem2Cfg<16, 32, 8>::LDS);
+  static const char* ev = getenv("YDBL_STEM2_TH");  // A/B knob (read once per process): 4 / 16-row tiles
+  const int th = ev && *ev ? atoi(ev) : 8;
+#define YDBL_STEM2_GO(C0_, TH_)                                                                                     \
+  return v4 ? go(stem2_kernel<C0_, 32, TH_, true>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)                           \
+            : go(stem2_kernel<C0_, 32, TH_, false>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)
+  if (c0 == 8 && th == 4) YDBL_STEM2_GO(8, 4);
+  if (c0 == 8 && th == 16) YDBL_STEM2_GO(8, 16);
+  if (c0 == 8) YDBL_STEM2_GO(8, 8);
+  if (c0 == 16) YDBL_STEM2_GO(16, 8);
+#undef YDBL_STEM2_GO
   return fail(YDBL_EINVAL, "stem2: c0 must be 8 or 16");
 }

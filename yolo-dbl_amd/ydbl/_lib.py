@@ -49,12 +49,6 @@ class DsConvDesc(C.Structure):
                 ("g2_x", View), ("g2_y", View), ("g2_act", C.c_int32)]
 
 
-class DsBneckDesc(C.Structure):
-    _fields_ = [("x", View), ("y", View), ("dw1_w", C.c_void_p), ("pw1_w", C.c_void_p), ("b1", C.c_void_p),
-                ("dw2_w", C.c_void_p), ("pw2_w", C.c_void_p), ("b2", C.c_void_p), ("kpad", C.c_int32),
-                ("add", C.c_int32)]
-
-
 class HgDesc(C.Structure):
     _fields_ = [("x", View), ("xp", View), ("y", View), ("num_edges", C.c_int32), ("num_heads", C.c_int32),
                 ("proto_base", C.c_void_p), ("ctx_w", C.c_void_p), ("ctx_b", C.c_void_p),
@@ -131,7 +125,6 @@ SIGNATURES = {
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_pair_nhwc": ([C.POINTER(DwConvDesc), C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dsconv_nhwc": ([C.POINTER(DsConvDesc), _P], C.c_int),
-    "ydbl_dsbottleneck_nhwc": ([C.POINTER(DsBneckDesc), _P], C.c_int),
     "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
     "ydbl_conv_stem": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _P, _P, C.c_int32, C.c_int32,
                         C.c_int32, _VP, _P], C.c_int),

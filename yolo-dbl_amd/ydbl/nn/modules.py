@@ -596,19 +596,6 @@ class DSBottleneck(nn.Module):
         self.cv2 = DSConv(c_, c2, k2, s=1, p=None, d=d2)
         self.add = shortcut and c1 == c2
 
-    def fused_ok(self, plan, x, y) -> bool:
-        """cv1 -> cv2 as one ydbl_dsbottleneck_nhwc launch: fp16, C = 64 in and out, k 3 then 7 (dil 1).
-        Opt-in (YDBL_DSBNECK=1): at DBL-n's 40^2 bs32 the fused launch (40.7 us) is slower than the two
-        DSConv launches (27.7 us, scripts/dsb_bench.py) -- the 3x recomputed 3x3 depthwise and the 7x7
-        depthwise make it VALU/LDS-bound at 2 workgroups per CU."""
-        a, b = self.cv1, self.cv2
-        return (plan.dtype == torch.float16 and os.environ.get("YDBL_DSBNECK") == "1" and x.c == 64
-                and a.dw.in_channels == a.pw.out_channels == b.pw.out_channels == 64
-                and a.dw.kernel_size == (3, 3) and b.dw.kernel_size == (7, 7)
-                and a.dw.stride == b.dw.stride == (1, 1) and a.dw.dilation == b.dw.dilation == (1, 1)
-                and a.dw.bias is None and b.dw.bias is None and x.cs % 8 == 0 and y.cs % 8 == 0
-                and (y.base is not x.base or y.off + y.c <= x.off or x.off + x.c <= y.off))
-
     def emit(self, plan, x, out=None, cv3=None):
         """cv3 = (C3's cv3 Conv, its second input view (the cv2 branch), its output view or None): the DSC3k's
         cv3 as the trailing GEMM of this bottleneck's k7 DSConv; returns cv3's output then."""
@@ -623,23 +610,6 @@ class DSBottleneck(nn.Module):
                         _lib.RES_ADD if self.add else _lib.RES_NONE,
                         g2=(w3.reshape(w3.shape[0], -1), b3, x2, o3, _act_code(conv3.act)))
             return o3
-        if self.fused_ok(plan, x, y):
-            keep = []
-
-            def dsconv_params(m):
-                w, b = fold_bn(m.pw.weight, m.pw.bias, m.bn)
-                dw = plan.const(m.dw.weight.detach().float().cpu().reshape(64, 9 if m.dw.kernel_size[0] == 3 else 49)
-                                .t().contiguous())
-                pw = plan.const(w.reshape(64, 64).to(torch.float16))
-                bd = plan.const(b.float())
-                keep.extend([dw, pw, bd])
-                return dw.data_ptr(), pw.data_ptr(), bd.data_ptr()
-
-            d1, p1, b1 = dsconv_params(self.cv1)
-            d2, p2, b2 = dsconv_params(self.cv2)
-            desc = _lib.DsBneckDesc(x.struct(), y.struct(), d1, p1, b1, d2, p2, b2, 64, int(self.add))
-            plan.launch("ydbl_dsbottleneck_nhwc", desc, what="DSBottleneck.k3k7", keep=[desc, *keep])
-            return y
         t = self.cv1.emit(plan, x)
         return self.cv2.emit(plan, t, y, res=x if self.add else None,
                              res_mode=_lib.RES_ADD if self.add else _lib.RES_NONE)
