@@ -247,11 +247,11 @@ int64_t ydbl_hg_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges)
 int ydbl_hg_context(const ydbl_hg_desc* d, void* stream);
 /* stage 2: logits, softmax over tokens, vertex->edge->vertex, residual (needs xp) */
 int ydbl_hg_propagate(const ydbl_hg_desc* d, void* stream);
-/* The whole AdaHGConv (block.py:1582-1708, pre_head_proj included: xp unused, pre_w/pre_b set) in one launch,
- * one 1024-thread workgroup per image with the N x E logits in LDS; head_dim 16, (dim, edges) in
- * {64, 128} x {4, 8}, ydbl_hg_fused_lds() <= 160 KiB (else: ydbl_hg_context + conv + ydbl_hg_propagate).
- * No workspace. */
-int64_t ydbl_hg_fused_lds(int32_t tokens, int32_t dim, int32_t edges, int32_t dtype);
+/* The whole AdaHGConv (block.py:1582-1708, pre_head_proj included: xp unused, pre_w/pre_b set) as three kernels
+ * over (64-token slice, image) workgroups, the per-image reductions merged in-launch by each image's last slice;
+ * head_dim 16, (dim, edges) in {64, 128} x {4, 8}.  workspace: ydbl_hg_fused_workspace() bytes, ZEROED once by
+ * the caller (its arrival counters are left zeroed again after every call); -1 = unsupported shape. */
+int64_t ydbl_hg_fused_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges, int32_t dtype);
 int ydbl_hg_fused(const ydbl_hg_desc* d, void* stream);
 
 /* Detect decode + NMS candidate extraction.

@@ -32,6 +32,35 @@ struct ConvArgs {
   T* g2y; int g2ycs; int g2act;
 };
 
+// ---- in-launch hand-off of per-workgroup partials (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1
+// slab recipe of cdna_hip_programming.md's split-K item): every workgroup stores its fp32 partials WRITE-THROUGH
+// (sc1 buffer stores), every storing wave drains them, one relaxed agent-scope ticket per workgroup; the
+// workgroup that draws the last ticket reads every slab with sc1 loads (L1 bypassed).  No __threadfence(): its
+// L2 write-back + invalidate in every workgroup cost 6x on a split-K conv.
+using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
+using gint = __attribute__((address_space(1))) int;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+}
+__device__ __forceinline__ void slab_store(__amdgpu_buffer_rsrc_t r, int off, const f32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);  // aux 16 = sc1
+}
+__device__ __forceinline__ f32x4 slab_load(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+// after this workgroup's slab stores: true (in every thread) when it drew the last of `nsplit` tickets
+__device__ __forceinline__ bool splitk_arrive(gint* cnt, int nsplit, int* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0)
+    *lds_flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
+  __syncthreads();
+  return *lds_flag != 0;
+}
+__device__ __forceinline__ void splitk_reset(gint* cnt) {  // ready for the next launch (graph replay)
+  __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------
 template <typename T, bool Q8> struct Op {
   using lds = typename Vec<T>::type;

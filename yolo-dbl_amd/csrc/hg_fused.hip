@@ -1,329 +1,435 @@
-// AdaHGConv in ONE launch per call (U/nn/modules/block.py:1582-1708: AdaHyperedgeGen + AdaHGConv), for token
-// counts whose N x E logits fit in LDS (every DBL-n / DBL-s call at 640: N = 1600 tokens, D = 64 / 128,
-// E = 4 / 8, head_dim 16).  hg.hip runs the same math as seven launches (stats, proto, the pre_head_proj
-// 1x1 conv, logits, gather, edge, out) of a few microseconds of work each; here one workgroup of 1024
-// threads owns one image and keeps everything between the passes on the CU:
-//   pass 1  ctx = [mean_N X | max_N X]: threads (8-channel vector, token lane) sweep X, wave shuffles +
-//           a 16-wave LDS combine; proto = base + Wc ctx + bc  -> LDS [E][D] fp32;
-//   pass 2  xp = X Wp^T + bp on MFMA, one 16-token tile per wave step with the B fragments loaded straight
-//           from X (no LDS staging, no barrier), rounded to the activation dtype as the unfused conv stores
-//           it; logits[n][e] = mean_h (xp_h[n] . proto_h[e]) / sqrt(16) -> LDS [N][E] fp32 (each 16-channel
-//           output tile of the MFMA is one head);
-//   softmax over N per hyperedge (max, sum of exp) -> A[n][e] in place;
-//   pass 3  He = A^T X (threads as pass 1, per-thread accumulators, shuffle + LDS combine in fixed order);
-//           He2 = GELU(He We^T + be), He3 = He2 Wn^T (node_proj re-associated as in hg.hip);
-//   pass 4  y[n] = GELU(A[n] He3 + bn) + X[n].
-// X is read four times, from L2 (one image is 200-400 KB); the workgroup runs beside the other sub-batch
-// stream's kernels on the remaining CUs.  All arithmetic fp32; reduction orders differ from hg.hip's
-// (tests/test_gpu_ops.py compares both with the oracle, and with each other).
+// AdaHGConv (U/nn/modules/block.py:1582-1708: AdaHyperedgeGen + AdaHGConv, pre_head_proj included) in four
+// launches spread over the chip (every DBL call: N = 1600 tokens at 640, D = 64 / 128, E = 4 / 8, head_dim 16).
+// The math has three reductions over all N tokens of an image (context stats, softmax over N, He = A^T X);
+// each launch splits the tokens into slices of HG3_TS, one 256-thread workgroup per (slice, image), and the
+// workgroup that finishes an image's reduction last (sc1 slab hand-off, conv_common.hpp) runs the small
+// per-image tail:
+//   hg3_ctx   partial [sum | max] of X per slice -> last: ctx;
+//   hg3_proto proto = base + Wc ctx + bc (16 rows per workgroup: the 2D x E*D weight is read by many CUs at once);
+//   hg3_edge  xp = X Wp^T + bp (MFMA, rounded as the unfused conv stores it), logits = mean_h(xp_h . proto_h) / 4
+//             (kept in the workspace), per-slice online-softmax partials (max m_s, sum of exp, He'_s =
+//             sum exp(l - m_s) X) -> last: m, 1/S, He = sum_s e^(m_s - m) He'_s / S, He2 = GELU(He We^T + be),
+//             He3 = He2 Wn^T (node_proj re-associated);
+//   hg3_out   y = GELU(A He3 + bn) + X, A = exp(l - m) / S.
+// (One 1024-thread workgroup per image doing all of it -- the previous form -- kept 16 CUs busy for 58 us per
+// call at bs16 while the rest of the chip waited.)  All arithmetic fp32; slices merge in slice order.
 #include "conv_common.hpp"
 
 namespace ydbl {
 
-constexpr int HGF_NT = 1024, HGF_WAVES = HGF_NT / 64;
-constexpr int64_t HGF_LDS_MAX = 160 * 1024 - 1024;  // dynamic LDS cap (the kernel's static s_stat stays inside)
+constexpr int HG3_TS = 64;  // tokens per slice (a 16-token MFMA tile per wave)
+constexpr int HG3_ZB = 8;   // slab loads issued together by a merging thread
+constexpr int HG3_NSMAX = 128;  // slices per image the merge handles (N <= 8192 tokens)
 
 template <typename T, int D, int E>
-struct HgfCfg {
-  static constexpr int V = Vec<T>::N;           // channels per 16-byte vector
-  static constexpr int CV = D / V;              // vectors per token
-  static constexpr int TL = HGF_NT / CV;        // token lanes
-  static constexpr int TLW = 64 / CV;           // token lanes per wave
-  static constexpr int NTC = D / 16;            // 16-channel tiles = heads (head_dim 16)
-  static constexpr int KS = D / (4 * V);        // MFMA k-steps over D (32 f16 / 16 f32 channels each)
+struct Hg3 {
+  static constexpr int V = Vec<T>::N;  // channels per 16-byte vector
+  static constexpr int CV = D / V;     // vectors per token
+  static constexpr int TL = 256 / CV;  // token lanes of a workgroup
+  static constexpr int NTC = D / 16;   // 16-channel output tiles = heads (head_dim 16)
+  static constexpr int KS = D / (4 * V);
+  static constexpr int R2 = (2 * E + E * D + 3) / 4 * 4;  // floats of a slice's edge-stage partial
 };
 
-// LDS bytes: logits [N][E] + Wp [D][D] (T) + proto, He, He2/He3 [E][D] + combine scratch [16][max(2D, 4D)]
-template <typename T, int D, int E>
-constexpr int64_t hgf_lds(int N) {
-  return (int64_t)N * E * 4 + (int64_t)D * D * sizeof(T) + 3LL * E * D * 4 + (int64_t)HGF_WAVES * 4 * D * 4 + 256;
+// workspace carve-up (bytes, 256-aligned sections)
+struct Hg3Ws {
+  int64_t cnt, slab1, ctx, proto, logits, slab2, he3, stat, total;
+};
+static Hg3Ws hg3_ws(int B, int N, int D, int E) {
+  auto up = [](int64_t v) { return (v + 255) & ~255ll; };
+  const int NS = (N + HG3_TS - 1) / HG3_TS, R2 = (2 * E + E * D + 3) / 4 * 4;
+  Hg3Ws w;
+  w.cnt = 0;
+  w.slab1 = up(w.cnt + 2LL * B * 4);
+  w.ctx = up(w.slab1 + (int64_t)B * NS * 2 * D * 4);
+  w.proto = up(w.ctx + (int64_t)B * 2 * D * 4);
+  w.logits = up(w.proto + (int64_t)B * E * D * 4);
+  w.slab2 = up(w.logits + (int64_t)B * N * E * 4);
+  w.he3 = up(w.slab2 + (int64_t)B * NS * R2 * 4);
+  w.stat = up(w.he3 + (int64_t)B * E * D * 4);
+  w.total = up(w.stat + (int64_t)B * 2 * E * 4);
+  return w;
 }
 
+// ---- 1. context [mean_N X | max_N X] and the prototypes
 template <typename T, int D, int E>
-__global__ __launch_bounds__(HGF_NT, 1) void hg_fused_kernel(DView<const T> x, DView<T> y, int N, int H,
-                                                              const float* __restrict__ base,
-                                                              const float* __restrict__ wc, const float* __restrict__ bc,
-                                                              const T* __restrict__ wp, const float* __restrict__ bp,
-                                                              const float* __restrict__ we, const float* __restrict__ be,
-                                                              const float* __restrict__ wn,
-                                                              const float* __restrict__ bn) {
-  using C = HgfCfg<T, D, E>;
-  constexpr int V = C::V, CV = C::CV, TL = C::TL, TLW = C::TLW, NTC = C::NTC, KS = C::KS;
-  using vec = typename Vec<T>::type;
-  extern __shared__ __align__(16) unsigned char smem[];
-  float* s_l = reinterpret_cast<float*>(smem);                    // [N][E] logits, then A
-  T* s_wp = reinterpret_cast<T*>(s_l + (int64_t)N * E);           // [D][D] pre_head_proj weight
-  float* s_p = reinterpret_cast<float*>(s_wp + D * D);            // [E][D] proto
-  float* s_he = s_p + E * D;                                      // [E][D] He, then He3
-  float* s_h2 = s_he + E * D;                                     // [E][D] He2
-  float* s_red = s_h2 + E * D;                                    // [16 waves][4 * D] combine scratch
-  __shared__ float s_stat[2][E];
-
+__global__ __launch_bounds__(256) void hg3_ctx_kernel(DView<const T> x, int N, unsigned char* __restrict__ ws, Hg3Ws o) {
+  using C = Hg3<T, D, E>;
+  constexpr int V = C::V, CV = C::CV, TL = C::TL;
+  __shared__ float s_red[4 * 2 * D];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int b = blockIdx.x;
+  const int sl = blockIdx.x, b = blockIdx.y, NS = gridDim.x;
+  const int cv = tid % CV, tl = tid / CV;
   const T* xb = x.p + (int64_t)b * N * x.cs;
-  const int cv = tid % CV, tl = tid / CV;  // pass 1 / 3 / 4 thread roles
-
-  for (int i = tid; i < D * D / V; i += HGF_NT) reinterpret_cast<vec*>(s_wp)[i] = reinterpret_cast<const vec*>(wp)[i];
-
-  // ---------------------------------------------------------------- pass 1: context + prototypes
-  {
-    float s[V], m[V];
+  const int n0 = sl * HG3_TS, n1 = min(N, n0 + HG3_TS);
+  float sm[V], mx[V];
 #pragma unroll
-    for (int q = 0; q < V; ++q) { s[q] = 0.f; m[q] = -INFINITY; }
-#pragma unroll 4
-    for (int n = tl; n < N; n += TL) {
-      float v[V];
-      load_f<V>(xb + (int64_t)n * x.cs + cv * V, v);
+  for (int q = 0; q < V; ++q) sm[q] = 0.f, mx[q] = -INFINITY;
+  for (int n = n0 + tl; n < n1; n += TL) {
+    float v[V];
+    load_f<V>(xb + (int64_t)n * x.cs + cv * V, v);
 #pragma unroll
-      for (int q = 0; q < V; ++q) { s[q] += v[q]; m[q] = fmaxf(m[q], v[q]); }
-    }
-#pragma unroll
-    for (int off = CV; off < 64; off <<= 1)
-#pragma unroll
-      for (int q = 0; q < V; ++q) { s[q] += __shfl_xor(s[q], off); m[q] = fmaxf(m[q], __shfl_xor(m[q], off)); }
-    if (lane < CV)
-#pragma unroll
-      for (int q = 0; q < V; ++q) {
-        s_red[wave * 4 * D + cv * V + q] = s[q];
-        s_red[wave * 4 * D + D + cv * V + q] = m[q];
-      }
-    __syncthreads();
-    float* ctx = s_h2;  // [2D] (E >= 2: fits in He2's slot until pass 3)
-    if (tid < 2 * D) {
-      float v = s_red[tid];
-      for (int w = 1; w < HGF_WAVES; ++w) v = tid < D ? v + s_red[w * 4 * D + tid] : fmaxf(v, s_red[w * 4 * D + tid]);
-      ctx[tid] = tid < D ? v / float(N) : v;
-    }
-    __syncthreads();
-    for (int o = tid; o < E * D; o += HGF_NT) {  // proto[o] = base[o] + (Wc[o] . ctx + bc[o])
-      const float* wr = wc + (int64_t)o * 2 * D;
-      float acc = 0.f;
-#pragma unroll 8
-      for (int k = 0; k < 2 * D; k += 4) {
-        const f32x4 w4 = *reinterpret_cast<const f32x4*>(wr + k);
-        acc = fmaf(w4[0], ctx[k], acc);
-        acc = fmaf(w4[1], ctx[k + 1], acc);
-        acc = fmaf(w4[2], ctx[k + 2], acc);
-        acc = fmaf(w4[3], ctx[k + 3], acc);
-      }
-      s_p[o] = base[o] + (acc + bc[o]);
-    }
-    __syncthreads();
+    for (int q = 0; q < V; ++q) sm[q] += v[q], mx[q] = fmaxf(mx[q], v[q]);
   }
-
-  // ---------------------------------------------------------------- pass 2: xp (MFMA) -> logits
-  {
-    const int g = lane >> 4, r16 = lane & 15;
-    const float inv_scale = 0.25f;  // 1 / sqrt(head_dim 16)
-    float bq[NTC][4], pq[NTC][E][4];  // this lane's 4 output channels of each tile: bias and prototype values
 #pragma unroll
-    for (int ct = 0; ct < NTC; ++ct)
+  for (int off = CV; off < 64; off <<= 1)
+#pragma unroll
+    for (int q = 0; q < V; ++q) sm[q] += __shfl_xor(sm[q], off), mx[q] = fmaxf(mx[q], __shfl_xor(mx[q], off));
+  if (lane < CV)
+#pragma unroll
+    for (int q = 0; q < V; ++q) s_red[wave * 2 * D + cv * V + q] = sm[q], s_red[wave * 2 * D + D + cv * V + q] = mx[q];
+  __syncthreads();
+  f32x4* slab = reinterpret_cast<f32x4*>(ws + o.slab1) + ((int64_t)b * NS + sl) * (2 * D / 4);
+  if (tid < 2 * D / 4) {  // 4 channels of [sum | max] per thread, the 4 waves combined in order
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * tid + e;
+      float a = s_red[c];
+      for (int w = 1; w < 4; ++w) a = c < D ? a + s_red[w * 2 * D + c] : fmaxf(a, s_red[w * 2 * D + c]);
+      v[e] = a;
+    }
+    slab[tid] = v;
+  }
+}
+
+// ---- 1b. ctx = [mean | max] of the image's slice partials (slice order), then proto[e][d] = base + (Wc[e*D+d] .
+// ctx + bc): 16 rows per workgroup, 4 per wave, every row's weights loaded in one round trip together with the
+// partials (lane l holds k = l*KL .. +KL-1), reduced across the wave
+template <int D, int E>
+__global__ __launch_bounds__(256) void hg3_proto_kernel(int N, int NS, const unsigned char* __restrict__ ws, Hg3Ws o,
+                                                        const float* __restrict__ base, const float* __restrict__ wc,
+                                                        const float* __restrict__ bc, unsigned char* __restrict__ wsw) {
+  constexpr int KL = 2 * D / 64;  // ctx entries per lane (2 or 4)
+  constexpr int C4 = 2 * D / 4;   // f32x4 columns of a slice partial
+  constexpr int ZG = 256 / C4;    // slice groups
+  __shared__ f32x4 s_part[ZG][C4];
+  __shared__ float s_ctx[2 * D];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.y;
+  float wv[4][KL];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) load_f<KL>(wc + (int64_t)(blockIdx.x * 16 + wave * 4 + r) * 2 * D + lane * KL, wv[r]);
+  const f32x4* slab = reinterpret_cast<const f32x4*>(ws + o.slab1) + (int64_t)b * NS * C4;
+  const int col = tid % C4, zg = tid / C4;
+  const bool sum = 4 * col < D;
+  f32x4 acc = sum ? f32x4{0.f, 0.f, 0.f, 0.f} : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int z0 = zg; z0 < NS; z0 += ZG * HG3_ZB) {
+    f32x4 v[HG3_ZB];
+#pragma unroll
+    for (int u = 0; u < HG3_ZB; ++u) v[u] = slab[(int64_t)min(z0 + u * ZG, NS - 1) * C4 + col];
+#pragma unroll
+    for (int u = 0; u < HG3_ZB; ++u) {
+      if (z0 + u * ZG >= NS) break;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[e] = sum ? acc[e] + v[u][e] : fmaxf(acc[e], v[u][e]);
+    }
+  }
+  s_part[zg][col] = acc;
+  __syncthreads();
+  if (tid < C4) {
+    f32x4 a = s_part[0][tid];
+    for (int g = 1; g < ZG; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) a[e] = sum ? a[e] + s_part[g][tid][e] : fmaxf(a[e], s_part[g][tid][e]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s_ctx[4 * tid + e] = sum ? a[e] / float(N) : a[e];
+  }
+  __syncthreads();
+  float cv[KL];
+#pragma unroll
+  for (int k = 0; k < KL; ++k) cv[k] = s_ctx[lane * KL + k];
+  float* proto = reinterpret_cast<float*>(wsw + o.proto) + (int64_t)b * E * D;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < KL; ++k) a = fmaf(wv[r][k], cv[k], a);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) a += __shfl_xor(a, off);
+    const int i = blockIdx.x * 16 + wave * 4 + r;
+    if (lane == 0) proto[i] = base[i] + (a + bc[i]);
+  }
+}
+
+// ---- 2. logits, online-softmax partials, He = A^T X, He2, He3
+template <typename T, int D, int E>
+__global__ __launch_bounds__(256) void hg3_edge_kernel(DView<const T> x, int N, int H, unsigned char* __restrict__ ws,
+                                                       Hg3Ws o, const T* __restrict__ wp, const float* __restrict__ bp,
+                                                       const float* __restrict__ we, const float* __restrict__ be,
+                                                       const float* __restrict__ wn) {
+  using C = Hg3<T, D, E>;
+  constexpr int V = C::V, CV = C::CV, TL = C::TL, NTC = C::NTC, KS = C::KS, R2 = C::R2;
+  using vec = typename Vec<T>::type;
+  __shared__ T s_wp[D * D];            // pre_head_proj weight [D][D]
+  __shared__ float s_l[HG3_TS * E];    // this slice's logits, then exp(l - m_s)
+  __shared__ float s_red[E * D];       // He'_s
+  __shared__ T s_xt[HG3_TS * D];       // the slice's tokens (B operand of the He' MFMA)
+  __shared__ float s_p[E * D];         // the image's prototypes
+  __shared__ float s_m[2][E];          // slice max, sum
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int sl = blockIdx.x, b = blockIdx.y, NS = gridDim.x;
+  const T* xb = x.p + (int64_t)b * N * x.cs;
+  const int n0 = sl * HG3_TS, ntok = min(N - n0, HG3_TS);
+  // every global load of the workgroup is issued before the first barrier: the weight tile, this wave's MFMA
+  // operands, this thread's He' token vectors, the prototypes
+  for (int i = tid; i < D * D / V; i += 256) reinterpret_cast<vec*>(s_wp)[i] = reinterpret_cast<const vec*>(wp)[i];
+  const int tok = wave * 16 + r16;  // HG3_TS = 4 waves x 16 tokens
+  const bool tok_ok = tok < ntok;
+  vec bf[KS];
+#pragma unroll
+  for (int m = 0; m < KS; ++m) bf[m] = vload_sel(xb + (int64_t)(n0 + tok) * x.cs + m * 4 * V + g * V, xb, tok_ok);
+  constexpr int XT = HG3_TS / TL;  // He' tokens per thread
+  const int hcv = tid % CV, htl = tid / CV;
+  vec xh[XT];
+#pragma unroll
+  for (int u = 0; u < XT; ++u) {
+    const int t = htl + u * TL;
+    xh[u] = vload_sel(xb + (int64_t)(n0 + t) * x.cs + hcv * V, xb, t < ntok);
+  }
+  const float* proto = reinterpret_cast<const float*>(ws + o.proto) + (int64_t)b * E * D;
+#pragma unroll
+  for (int u = 0; u < XT; ++u) *reinterpret_cast<vec*>(&s_xt[(htl + u * TL) * D + hcv * V]) = xh[u];
+  for (int i = tid; i < E * D / 4; i += 256) reinterpret_cast<f32x4*>(s_p)[i] = reinterpret_cast<const f32x4*>(proto)[i];
+  float bq[NTC][4];
+#pragma unroll
+  for (int ct = 0; ct < NTC; ++ct)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[ct][q] = bp[ct * 16 + 4 * g + q];
+  __syncthreads();
+
+  // xp tile of wave `wave` (16 tokens) -> logits
+  {
+    const bool ok = tok_ok;
+    float tot[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) tot[e] = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < NTC; ++ct) {  // tile ct = head ct: its 16 channels are the 4 lanes g x 4 regs
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < KS; ++m) {
+        const vec af = *reinterpret_cast<const vec*>(s_wp + (ct * 16 + r16) * D + m * 4 * V + g * V);
+        acc = mfma_chunk<T>(af, bf[m], acc);
+      }
+      float hd[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) hd[e] = 0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int c = ct * 16 + 4 * g + q;
-        bq[ct][q] = bp[c];
+        const float xv = round_to<T>(acc[q] + bq[ct][q]);  // xp as the unfused conv stores it
 #pragma unroll
-        for (int e = 0; e < E; ++e) pq[ct][e][q] = s_p[e * D + c];
+        for (int e = 0; e < E; ++e) hd[e] = fmaf(xv, s_p[e * D + ct * 16 + 4 * g + q], hd[e]);
       }
-    float lmax[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) lmax[e] = -INFINITY;
-    const int ntt = (N + 15) / 16;
-    for (int tt = wave; tt < ntt; tt += HGF_WAVES) {
-      const int tok = tt * 16 + r16;
-      const bool ok = tok < N;
-      vec bf[KS];
-#pragma unroll
-      for (int m = 0; m < KS; ++m) bf[m] = vload_sel(xb + (int64_t)tok * x.cs + m * 4 * V + g * V, xb, ok);
-      f32x4 acc[NTC];
-#pragma unroll
-      for (int ct = 0; ct < NTC; ++ct) {
-        acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int m = 0; m < KS; ++m) {
-          const vec af = *reinterpret_cast<const vec*>(s_wp + (ct * 16 + r16) * D + m * 4 * V + g * V);
-          acc[ct] = mfma_chunk<T>(af, bf[m], acc[ct]);
-        }
-      }
-      float tot[E];
-#pragma unroll
-      for (int e = 0; e < E; ++e) tot[e] = 0.f;
-#pragma unroll
-      for (int ct = 0; ct < NTC; ++ct) {  // tile ct = head ct: its 16 channels are the 4 lanes g x 4 regs
-        float hd[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) hd[e] = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const float xv = round_to<T>(acc[ct][q] + bq[ct][q]);  // xp as the unfused conv stores it
-#pragma unroll
-          for (int e = 0; e < E; ++e) hd[e] = fmaf(xv, pq[ct][e][q], hd[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          hd[e] += __shfl_xor(hd[e], 16);
-          hd[e] += __shfl_xor(hd[e], 32);
-          tot[e] += hd[e] * inv_scale;
-        }
-      }
-      if (g == 0 && ok) {
-#pragma unroll
-        for (int e = 0; e < E; ++e) {
-          const float l = tot[e] / float(H);
-          s_l[tok * E + e] = l;
-          lmax[e] = fmaxf(lmax[e], l);
-        }
-      }
-    }
-    // softmax over tokens: max, then sum exp(l - max)
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) lmax[e] = fmaxf(lmax[e], __shfl_xor(lmax[e], off));
-    if (lane == 0)
-#pragma unroll
-      for (int e = 0; e < E; ++e) s_red[wave * E + e] = lmax[e];
-    __syncthreads();
-    if (tid < E) {
-      float m = s_red[tid];
-      for (int w = 1; w < HGF_WAVES; ++w) m = fmaxf(m, s_red[w * E + tid]);
-      s_stat[0][tid] = m;
-    }
-    __syncthreads();
-    float ps[E];
-#pragma unroll
-    for (int e = 0; e < E; ++e) ps[e] = 0.f;
-    for (int n = tid; n < N; n += HGF_NT)
-#pragma unroll
-      for (int e = 0; e < E; ++e) ps[e] += expf(s_l[n * E + e] - s_stat[0][e]);
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int off = 1; off < 64; off <<= 1) ps[e] += __shfl_xor(ps[e], off);
-    __syncthreads();  // s_red's max partials consumed
-    if (lane == 0)
-#pragma unroll
-      for (int e = 0; e < E; ++e) s_red[wave * E + e] = ps[e];
-    __syncthreads();
-    if (tid < E) {
-      float sum = s_red[tid];
-      for (int w = 1; w < HGF_WAVES; ++w) sum += s_red[w * E + tid];
-      s_stat[1][tid] = 1.0f / sum;
-    }
-    __syncthreads();
-    for (int i = tid; i < N * E; i += HGF_NT) {
-      const int e = i % E;
-      s_l[i] = expf(s_l[i] - s_stat[0][e]) * s_stat[1][e];
-    }
-    __syncthreads();
-  }
-
-  // ---------------------------------------------------------------- pass 3: He = A^T X, He2, He3
-  {
-    float acc[E][V];
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int q = 0; q < V; ++q) acc[e][q] = 0.f;
-#pragma unroll 2
-    for (int n = tl; n < N; n += TL) {
-      float v[V];
-      load_f<V>(xb + (int64_t)n * x.cs + cv * V, v);
 #pragma unroll
       for (int e = 0; e < E; ++e) {
-        const float a = s_l[n * E + e];
-#pragma unroll
-        for (int q = 0; q < V; ++q) acc[e][q] = fmaf(a, v[q], acc[e][q]);
+        hd[e] += __shfl_xor(hd[e], 16);
+        hd[e] += __shfl_xor(hd[e], 32);
+        tot[e] += hd[e] * 0.25f;  // 1 / sqrt(head_dim 16)
       }
     }
+    float* lg = reinterpret_cast<float*>(ws + o.logits) + ((int64_t)b * N + n0) * E;
+    if (g == 0 && ok) {
 #pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int off = CV; off < 64; off <<= 1)
-#pragma unroll
-        for (int q = 0; q < V; ++q) acc[e][q] += __shfl_xor(acc[e][q], off);
-    for (int e0 = 0; e0 < E; e0 += 4) {  // combine the 16 waves' partials, 4 hyperedges at a time
-      if (lane < CV)
-#pragma unroll
-        for (int e = 0; e < 4 && e0 + e < E; ++e)
-#pragma unroll
-          for (int q = 0; q < V; ++q) s_red[wave * 4 * D + e * D + cv * V + q] = acc[e0 + e][q];
-      __syncthreads();
-      for (int i = tid; i < 4 * D && e0 + i / D < E; i += HGF_NT) {
-        float v = s_red[i];
-        for (int w = 1; w < HGF_WAVES; ++w) v += s_red[w * 4 * D + i];
-        s_he[e0 * D + i] = v;
+      for (int e = 0; e < E; ++e) {
+        const float l = tot[e] / float(H);
+        s_l[tok * E + e] = l;
+        lg[tok * E + e] = l;
       }
-      __syncthreads();
     }
-    // He2 = GELU(He We^T + be), then He3 = He2 Wn^T: a wave per weight row d (coalesced row loads, lanes over k),
-    // the E dot products reduced across the wave
-    auto rows = [&](const float* __restrict__ in, const float* __restrict__ w, float* out, const float* bias) {
-      for (int d = wave; d < D; d += HGF_WAVES) {
-        float sv[E];
-#pragma unroll
-        for (int e = 0; e < E; ++e) sv[e] = 0.f;
-#pragma unroll
-        for (int k = lane; k < D; k += 64) {
-          const float wv = w[(int64_t)d * D + k];
-#pragma unroll
-          for (int e = 0; e < E; ++e) sv[e] = fmaf(in[e * D + k], wv, sv[e]);
-        }
-#pragma unroll
-        for (int e = 0; e < E; ++e)
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) sv[e] += __shfl_xor(sv[e], off);
-        if (lane < E) {
-          float v = sv[0];
-#pragma unroll
-          for (int e = 1; e < E; ++e) v = lane == e ? sv[e] : v;
-          out[lane * D + d] = bias ? gelu_erf(v + bias[d]) : v;
-        }
-      }
-    };
-    rows(s_he, we, s_h2, be);
-    __syncthreads();
-    rows(s_h2, wn, s_he, nullptr);  // He3 over He's slot (He is dead)
-    __syncthreads();
   }
-
-  // ---------------------------------------------------------------- pass 4: y = GELU(A He3 + bn) + X
+  __syncthreads();
+  // slice max and sum of exp per hyperedge: a wave per hyperedge, a lane per token (HG3_TS = 64), butterflies
+  for (int e = wave; e < E; e += 4) {
+    const float l = lane < ntok ? s_l[lane * E + e] : -INFINITY;
+    float m = l;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    const float pe = lane < ntok ? expf(l - m) : 0.f;
+    if (lane < ntok) s_l[lane * E + e] = pe;
+    float sum = pe;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+    if (lane == 0) s_m[0][e] = m, s_m[1][e] = sum;
+  }
+  __syncthreads();
+  // He'_s[e][d] = sum_t exp(l_t - m_s) X_t[d] on the exact-f32 MFMA (16x16x4: the sequential fmaf chain over
+  // tokens, bitwise): A[e][t] = the slice's probabilities (rows e >= E zero), B[t][d] = X from the LDS tile; a
+  // wave per 16-channel column tile
   {
-    float h3[E][V], bv[V];
-#pragma unroll
-    for (int e = 0; e < E; ++e)
-#pragma unroll
-      for (int q = 0; q < V; ++q) h3[e][q] = s_he[e * D + cv * V + q];
-    load_f<V>(bn + cv * V, bv);
-    T* yb = y.p + (int64_t)b * N * y.cs;
-#pragma unroll 2
-    for (int n = tl; n < N; n += TL) {
-      float v[V], o[V];
-      load_f<V>(xb + (int64_t)n * x.cs + cv * V, v);
-#pragma unroll
-      for (int q = 0; q < V; ++q) {
-        float s = 0.f;
-#pragma unroll
-        for (int e = 0; e < E; ++e) s = fmaf(s_l[n * E + e], h3[e][q], s);
-        o[q] = gelu_erf(s + bv[q]) + v[q];
+    constexpr int NCT = D / 16;  // column tiles
+    for (int ct = wave; ct < NCT; ct += 4) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+      for (int t0 = 0; t0 < HG3_TS; t0 += 4) {
+        const int t = t0 + g;
+        const float av = (r16 < E && t < ntok) ? s_l[t * E + r16] : 0.f;
+        const float bv = t < ntok ? float(s_xt[t * D + ct * 16 + r16]) : 0.f;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc, 0, 0, 0);
       }
-      store_f<V>(yb + (int64_t)n * y.cs + cv * V, o);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * g + q < E) s_red[(4 * g + q) * D + ct * 16 + r16] = acc[q];
     }
+  }
+  __syncthreads();
+  f32x4* rec = reinterpret_cast<f32x4*>(ws + o.slab2) + ((int64_t)b * NS + sl) * (R2 / 4);
+  for (int i = tid; i < R2 / 4; i += 256) {  // record: [m_s (E) | S_s (E) | He'_s (E*D)]
+    f32x4 v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int f = 4 * i + e;
+      float a = 0.f;
+      if (f < E) a = s_m[0][f];
+      else if (f < 2 * E) a = s_m[1][f - E];
+      else if (f < 2 * E + E * D) {
+        a = s_red[f - 2 * E];
+      }
+      v[e] = a;
+    }
+    rec[i] = v;
+  }
+}
+
+// ---- 2b. per (image, hyperedge e): merge the slices (slice order) into He[e], then He2[e] = GELU(We He[e] + be),
+// He3[e] = Wn He2[e] (row e of each product depends on row e only).  Every load is issued before the first use:
+// a thread's two weight rows (output d = tid % D), the slices' (max, sum) of e, this thread's He' entries.
+template <int D, int E>
+__global__ __launch_bounds__(256) void hg3_merge_kernel(int NS, unsigned char* __restrict__ ws, Hg3Ws o,
+                                                        const float* __restrict__ we, const float* __restrict__ be,
+                                                        const float* __restrict__ wn) {
+  constexpr int R2 = (2 * E + E * D + 3) / 4 * 4;
+  constexpr int ZG = 256 / D;  // slice groups of the He' merge (4 at D 64, 2 at D 128)
+  constexpr int ZB = (HG3_NSMAX + ZG - 1) / ZG;
+  __shared__ float s_ms[2][HG3_NSMAX];
+  __shared__ float s_part[ZG][D];
+  __shared__ float s_v[2][D];
+  __shared__ float s_st[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int e = blockIdx.x, b = blockIdx.y;
+  const int d = tid % D, zg = tid / D;
+  const float* recs = reinterpret_cast<const float*>(ws + o.slab2) + (int64_t)b * NS * R2;
+  f32x4 w1[D / 4 / ZG], w2[D / 4 / ZG];  // this thread's quarter/half of weight rows d (k split over the ZG groups)
+#pragma unroll
+  for (int i = 0; i < D / 4 / ZG; ++i) {
+    w1[i] = reinterpret_cast<const f32x4*>(we + (int64_t)d * D)[zg * (D / 4 / ZG) + i];
+    w2[i] = reinterpret_cast<const f32x4*>(wn + (int64_t)d * D)[zg * (D / 4 / ZG) + i];
+  }
+  for (int z = tid; z < NS; z += 256) s_ms[0][z] = recs[(int64_t)z * R2 + e], s_ms[1][z] = recs[(int64_t)z * R2 + E + e];
+  float hv[ZB];
+#pragma unroll
+  for (int u = 0; u < ZB; ++u) {
+    const int z = min(zg + u * ZG, NS - 1);
+    hv[u] = recs[(int64_t)z * R2 + 2 * E + e * D + d];
+  }
+  __syncthreads();
+  if (wave == 0) {  // m, 1/S over the slices: lanes over slices, butterflies
+    float m = -INFINITY;
+    for (int z = lane; z < NS; z += 64) m = fmaxf(m, s_ms[0][z]);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    float S = 0.f;
+    for (int z = lane; z < NS; z += 64) S += s_ms[1][z] * expf(s_ms[0][z] - m);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) S += __shfl_xor(S, off);
+    if (lane == 0) s_st[0] = m, s_st[1] = 1.0f / S;
+  }
+  __syncthreads();
+  {
+    float a = 0.f;
+#pragma unroll
+    for (int u = 0; u < ZB; ++u) {
+      const int z = zg + u * ZG;
+      if (z < NS) a = fmaf(hv[u], expf(s_ms[0][z] - s_st[0]), a);
+    }
+    s_part[zg][d] = a;
+  }
+  __syncthreads();
+  if (tid < D) {
+    float a = s_part[0][tid];
+    for (int g = 1; g < ZG; ++g) a += s_part[g][tid];
+    s_v[0][tid] = a * s_st[1];  // He[e]
+  }
+  __syncthreads();
+  // the two GEMVs: thread (d, zg) dots its k range, the ZG partials summed in group order
+  auto gemv = [&](const f32x4 (&w)[D / 4 / ZG], const float* in) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < D / 4 / ZG; ++i) {
+      const int k = (zg * (D / 4 / ZG) + i) * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) a = fmaf(w[i][q], in[k + q], a);
+    }
+    s_part[zg][d] = a;
+    __syncthreads();
+    float r = 0.f;
+    if (tid < D) {
+      r = s_part[0][tid];
+      for (int g = 1; g < ZG; ++g) r += s_part[g][tid];
+    }
+    __syncthreads();
+    return r;
+  };
+  const float h2 = gemv(w1, s_v[0]);
+  if (tid < D) s_v[1][tid] = gelu_erf(h2 + be[tid]);
+  __syncthreads();
+  const float h3 = gemv(w2, s_v[1]);
+  if (tid < D) reinterpret_cast<float*>(ws + o.he3)[((int64_t)b * E + e) * D + tid] = h3;
+  float* st = reinterpret_cast<float*>(ws + o.stat) + (int64_t)b * 2 * E;
+  if (tid == 0) st[e] = s_st[0], st[E + e] = s_st[1];
+}
+
+// ---- 3. y = GELU(A He3 + bn) + X, A = exp(l - m) / S
+template <typename T, int D, int E>
+__global__ __launch_bounds__(256) void hg3_out_kernel(DView<const T> x, DView<T> y, int N,
+                                                      const unsigned char* __restrict__ ws, Hg3Ws o,
+                                                      const float* __restrict__ bn) {
+  using C = Hg3<T, D, E>;
+  constexpr int V = C::V, CV = C::CV, TL = C::TL;
+  const int tid = threadIdx.x, cv = tid % CV, tl = tid / CV;
+  const int b = blockIdx.y, n0 = blockIdx.x * HG3_TS, n1 = min(N, n0 + HG3_TS);
+  const float* he3 = reinterpret_cast<const float*>(ws + o.he3) + (int64_t)b * E * D;
+  const float* st = reinterpret_cast<const float*>(ws + o.stat) + (int64_t)b * 2 * E;
+  const float* lg = reinterpret_cast<const float*>(ws + o.logits) + (int64_t)b * N * E;
+  float h3[E][V], bv[V], m[E], inv[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    load_f<V>(he3 + e * D + cv * V, h3[e]);
+    m[e] = st[e];
+    inv[e] = st[E + e];
+  }
+  load_f<V>(bn + cv * V, bv);
+  const T* xb = x.p + (int64_t)b * N * x.cs;
+  T* yb = y.p + (int64_t)b * N * y.cs;
+  for (int n = n0 + tl; n < n1; n += TL) {
+    float v[V], ov[V], a[E];
+    load_f<V>(xb + (int64_t)n * x.cs + cv * V, v);
+#pragma unroll
+    for (int e = 0; e < E; ++e) a[e] = expf(lg[(int64_t)n * E + e] - m[e]) * inv[e];
+#pragma unroll
+    for (int q = 0; q < V; ++q) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int e = 0; e < E; ++e) sacc = fmaf(a[e], h3[e][q], sacc);
+      ov[q] = gelu_erf(sacc + bv[q]) + v[q];
+    }
+    store_f<V>(yb + (int64_t)n * y.cs + cv * V, ov);
   }
 }
 
 template <typename T, int D, int E>
 static int hgf_go(const ydbl_hg_desc* d, hipStream_t s) {
-  const int N = d->x.h * d->x.w;
-  const int64_t lds = hgf_lds<T, D, E>(N);
-  // Dynamic LDS up to the CU's 160 KiB launches without an opt-in on ROCm (measured: the 128-dim / 8-edge fp32
-  // instantiation at N = 1600 takes 158 KiB); hipFuncSetAttribute(MaxDynamicSharedMemorySize) returns an error
-  // there, which would otherwise surface in check_launch below, so it is not called.
-  hg_fused_kernel<T, D, E><<<d->x.n, HGF_NT, (size_t)lds, s>>>(
-      DView<const T>{reinterpret_cast<const T*>(d->x.ptr), d->x.n, d->x.h, d->x.w, d->x.c, d->x.cs}, dview<T>(d->y), N,
-      d->num_heads, d->proto_base, d->ctx_w, d->ctx_b, reinterpret_cast<const T*>(d->pre_w), d->pre_b, d->edge_w,
-      d->edge_b, d->node_w, d->node_b);
+  const int N = d->x.h * d->x.w, B = d->x.n;
+  const int NS = (N + HG3_TS - 1) / HG3_TS;
+  const Hg3Ws o = hg3_ws(B, N, D, E);
+  unsigned char* ws = reinterpret_cast<unsigned char*>(d->workspace);
+  const DView<const T> xv{reinterpret_cast<const T*>(d->x.ptr), d->x.n, d->x.h, d->x.w, d->x.c, d->x.cs};
+  hg3_ctx_kernel<T, D, E><<<dim3(NS, B), 256, 0, s>>>(xv, N, ws, o);
+  hg3_proto_kernel<D, E><<<dim3(E * D / 16, B), 256, 0, s>>>(N, NS, ws, o, d->proto_base, d->ctx_w, d->ctx_b, ws);
+  hg3_edge_kernel<T, D, E><<<dim3(NS, B), 256, 0, s>>>(xv, N, d->num_heads, ws, o, reinterpret_cast<const T*>(d->pre_w),
+                                                       d->pre_b, d->edge_w, d->edge_b, d->node_w);
+  hg3_merge_kernel<D, E><<<dim3(E, B), 256, 0, s>>>(NS, ws, o, d->edge_w, d->edge_b, d->node_w);
+  hg3_out_kernel<T, D, E><<<dim3(NS, B), 256, 0, s>>>(xv, dview<T>(d->y), N, ws, o, d->node_b);
   return check_launch("ydbl_hg_fused");
 }
 
@@ -344,12 +450,12 @@ static int hgf_dispatch(int dim, int e, bool f16, F&& f) {
 
 using namespace ydbl;
 
-extern "C" int64_t ydbl_hg_fused_lds(int32_t tokens, int32_t dim, int32_t edges, int32_t dtype) {
-  if (tokens < 1) return -1;
-  const int64_t r = hgf_dispatch(dim, edges, dtype == YDBL_F16, [&](auto T0, auto D0, auto E0) -> int {
-    return (int)hgf_lds<decltype(T0), decltype(D0)::value, decltype(E0)::value>(tokens);
-  });
-  return r;
+extern "C" int64_t ydbl_hg_fused_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges, int32_t dtype) {
+  if (n < 1 || tokens < 1) return -1;
+  const int64_t ok = hgf_dispatch(dim, edges, dtype == YDBL_F16, [&](auto, auto, auto) -> int { return 1; });
+  if (ok < 0) return -1;
+  if ((tokens + HG3_TS - 1) / HG3_TS > HG3_NSMAX) return -1;  // the merge's LDS holds <= HG3_NSMAX slices
+  return hg3_ws(n, tokens, dim, edges).total;
 }
 
 extern "C" int ydbl_hg_fused(const ydbl_hg_desc* d, void* stream) {
@@ -360,10 +466,10 @@ extern "C" int ydbl_hg_fused(const ydbl_hg_desc* d, void* stream) {
   if (!d->proto_base || !d->ctx_w || !d->ctx_b || !d->pre_w || !d->pre_b || !d->edge_w || !d->edge_b || !d->node_w ||
       !d->node_b)
     return fail(YDBL_EINVAL, "hg_fused: null weights");
+  if (!d->workspace) return fail(YDBL_EINVAL, "hg_fused: null workspace (ydbl_hg_fused_workspace bytes, zeroed once)");
   if (d->num_heads < 1 || d->x.c != 16 * d->num_heads) return fail(YDBL_EINVAL, "hg_fused: head_dim must be 16");
-  const int64_t lds = ydbl_hg_fused_lds(d->x.h * d->x.w, d->x.c, d->num_edges, d->x.dtype);
-  if (lds < 0) return fail(YDBL_EINVAL, "hg_fused: (dim, edges) must be (64|128, 4|8)");
-  if (lds > HGF_LDS_MAX) return fail(YDBL_EINVAL, "hg_fused: tokens x edges too large for LDS (use hg_context/propagate)");
+  if (ydbl_hg_fused_workspace(d->x.n, d->x.h * d->x.w, d->x.c, d->num_edges, d->x.dtype) < 0)
+    return fail(YDBL_EINVAL, "hg_fused: (dim, edges) must be (64|128, 4|8)");
   hipStream_t s = as_stream(stream);
   return hgf_dispatch(d->x.c, d->num_edges, d->x.dtype == YDBL_F16, [&](auto T0, auto D0, auto E0) -> int {
     return hgf_go<decltype(T0), decltype(D0)::value, decltype(E0)::value>(d, s);

@@ -139,7 +139,7 @@ SIGNATURES = {
     "ydbl_hg_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_hg_context": ([C.POINTER(HgDesc), _P], C.c_int),
     "ydbl_hg_propagate": ([C.POINTER(HgDesc), _P], C.c_int),
-    "ydbl_hg_fused_lds": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_hg_fused_workspace": ([C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32], C.c_int64),
     "ydbl_hg_fused": ([C.POINTER(HgDesc), _P], C.c_int),
     "ydbl_dysample2": ([C.POINTER(DySample2Desc), _P], C.c_int),
     "ydbl_detect_decode": ([C.POINTER(DecodeDesc), _P], C.c_int),

@@ -677,15 +677,17 @@ class AdaHGConv(nn.Module):
         p = [c(g.prototype_base.float()), c(g.context_net.weight.float()), c(g.context_net.bias.float()),
              c(self.edge_proj[0].weight.float()), c(self.edge_proj[0].bias.float()),
              c(self.node_proj[0].weight.float()), c(self.node_proj[0].bias.float())]
-        lds = _lib.lib.ydbl_hg_fused_lds(x.h * x.w, D, E, _lib.dtype_code(plan.dtype))
-        if (not os.environ.get("YDBL_HG_UNFUSED") and D == 16 * g.num_heads and 0 < lds <= 159 * 1024
+        nws = _lib.lib.ydbl_hg_fused_workspace(x.n, x.h * x.w, D, E, _lib.dtype_code(plan.dtype))
+        if (not os.environ.get("YDBL_HG_UNFUSED") and D == 16 * g.num_heads and nws > 0
                 and x.c == D and (y.base is not x.base or y.off + y.c <= x.off or x.off + x.c <= y.off)):
-            # the whole AdaHGConv, pre_head_proj included, in one launch per call (csrc/hg_fused.hip)
+            # the whole AdaHGConv, pre_head_proj included, from one C-ABI call (csrc/hg_fused.hip: three kernels
+            # over (token slice, image) workgroups)
             pw = c(g.pre_head_proj.weight.detach().float().to(plan.dtype).contiguous())
             pb = c(g.pre_head_proj.bias.detach().float())
-            d = HgDesc(x.struct(), _null_view(), y.struct(), E, g.num_heads, *[t.data_ptr() for t in p], None,
+            ws = plan.scratch(nws, zero=True)  # arrival counters start at zero; the kernels leave them there
+            d = HgDesc(x.struct(), _null_view(), y.struct(), E, g.num_heads, *[t.data_ptr() for t in p], ws.data_ptr(),
                        pw.data_ptr(), pb.data_ptr())
-            plan.launch("ydbl_hg_fused", d, what="AdaHG.fused", keep=[d, pw, pb, *p])
+            plan.launch("ydbl_hg_fused", d, what="AdaHG.fused", keep=[d, pw, pb, ws, *p])
             return y
         # X_proj = pre_head_proj(X) as a 1x1 conv over the token grid
         xp = plan.alloc(x.n, x.h, x.w, D)

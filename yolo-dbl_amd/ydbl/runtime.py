@@ -96,8 +96,8 @@ class Plan:
         self.bytes_allocated += t.numel() * t.element_size()
         return TV(t, 0, n, h, w, c, cs)
 
-    def scratch(self, nbytes: int) -> torch.Tensor:
-        t = torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+    def scratch(self, nbytes: int, zero: bool = False) -> torch.Tensor:
+        t = (torch.zeros if zero else torch.empty)(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
         self.buffers.append(t)
         self.bytes_allocated += t.numel()
         return t
