@@ -315,7 +315,8 @@ int ydbl_nms(const ydbl_nms_desc* d, void* stream);
  * from the NCHW fp32 batch x [n][3][h][w]; the full-resolution intermediate never leaves LDS.
  * params: device blob of ydbl_conv_stem2_params_size(c0) bytes filled on the HOST by
  * ydbl_conv_stem2_pack from fp32 weights w0 [c0][3][3][3], b0 [c0], w1 [2*c0][c0][3][3], b1 [2*c0]
- * (BN already folded); c0 = 8 or 16. */
+ * (BN already folded); c0 = 8 or 16.  The first conv's bias enters the MFMA as an fp16 weight on a constant-1 input
+ * slot (the reference's .half() bias), the second conv's is added in fp32. */
 typedef struct {
   const float* x;
   int32_t n, cin, h, w;

@@ -551,7 +551,7 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // once per column block, from L2/MALL at these map sizes).  Measured against 128-wide blocks on the
   // bench workloads: DBL-n bs32 14.82 -> 14.91 k img/s (bs16 graphs: 64->128 @80^2 22.6 -> 19.8 us,
   // 128->192 @40^2 15.6 -> 12.1 us), DBL-s bs64 7.52 -> 7.57 k, DBL-l 1280 bs8 467 -> 466 (noise).
-  const char* b64 = getenv("YDBL_IGEMM_BN64");  // A/B knob (read per launch): 0 = 128-wide column blocks
+  static const char* b64 = getenv("YDBL_IGEMM_BN64");  // A/B knob (read once per process): 0 = 128-wide column blocks
   if (!(b64 && *b64 == '0')) {
     if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
     if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);

@@ -161,7 +161,7 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
   // most CUs with one workgroup; 32-channel slices double the grid (conv_bench.py bs16: 384->64 @40^2
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
-  const char* ev = getenv("YDBL_HALO_N2");  // A/B knob (read per launch)
+  static const char* ev = getenv("YDBL_HALO_N2");  // A/B knob (read once per process)
   const int64_t n2_below = ev && *ev ? atoll(ev) : 400;
   if (a.Cout <= 32) {
     conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
@@ -195,7 +195,7 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   if (a.Cin % BK || a.Cin < 2 * BK || a.xcs % Vec<T>::N) return false;
   static const char* fth = getenv("YDBL_HALO_TH");  // A/B knob for scripts/conv_bench.py: force 4/8/16-row tiles
   const int force_th = fth && *fth ? atoi(fth) : 0;
-  const char* mp = getenv("YDBL_HALO_MINP");  // A/B knob (read per launch): smallest output-pixel count routed here
+  static const char* mp = getenv("YDBL_HALO_MINP");  // A/B knob (read once per process): smallest output-pixel count routed here
   // 51200 output pixels (40^2 x 32) was the measured crossover at bs32; the bench's two bs16 sub-batch
   // graphs put the 40^2 head convs at 25600, where the halo tile still wins (DBL-n bs32 on two streams
   // 13.7 k -> 14.1 k img/s; 12800 loses again: 14.0 k)
@@ -343,7 +343,7 @@ bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
   if (off || kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
   if (a.xcs % 8 || a.H != a.Ho || a.W != a.Wo || (int64_t)a.N * a.Ho * a.Wo >= (1LL << 31)) return false;
   if (a.Cin == 128 && a.Cout == 64) return launch_vw<128, 1, 4, 2>(a, 1, s), true;
-  const char* vm = getenv("YDBL_VW_MINP");  // A/B knob (read per launch)
+  static const char* vm = getenv("YDBL_VW_MINP");  // A/B knob (read once per process)
   const int64_t vw_min = vm && *vm ? atoll(vm) : 25601;
   if (a.Cin == 64 && a.Cout == 64 && a.P >= vw_min && a.P <= 65536) return launch_vw<64, 2, 2, 4>(a, 1, s), true;
   return false;

@@ -245,7 +245,7 @@ static int launch_ds(const ConvArgs<T>& a, const float* dww, const float* dwb, i
   // tiles, 1.7x the workgroups (DBL-n bs32 on two streams 13.98 k -> 14.45 k img/s; at bs32 / 480 tiles
   // the two are even, and the 16x8 tile stays ahead on DBL-s bs64 and DBL-l 1280)
   const int64_t t168 = (int64_t)a.N * cdiv(a.Ho, 16) * cdiv(a.Wo, 8);
-  const char* tl = getenv("YDBL_DS_T168");  // A/B knob (read per launch)
+  static const char* tl = getenv("YDBL_DS_T168");  // A/B knob (read once per process)
   const int64_t t168_max = tl && *tl ? atoll(tl) : 400;
   if (t == 'S' || (t == 'A' && a.Wo > 20 && t168 < t168_max)) launch_ds_tile<T, K, S, DIL, 8, 8, 2, false>(a, dww, dwb, dw_act, s);
   else if (a.Wo > 20 && t != '8') launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, dwb, dw_act, s);

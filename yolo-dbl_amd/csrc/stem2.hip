@@ -65,9 +65,11 @@ void stem2_pack(const float* w0, const float* b0, const float* w1, const float* 
       for (int j = 0; j < 8; ++j) {
         const int g = lane >> 4, row = lane & 15;
         const int k = 32 * m + 8 * g + j, q = k / 4, c = k % 4;
-        const bool live = q < 9 * Cfg::PS && q / 9 == row / Cfg::C0M && c < 3;
+        const bool live = q < 9 * Cfg::PS && q / 9 == row / Cfg::C0M;
         const int co = row % Cfg::C0M, tap = q % 9;
-        f0[(m * 64 + lane) * 8 + j] = (_Float16)(live ? w0[(co * 3 + c) * 9 + tap] : 0.f);
+        // slot 3 of a record is 1 for pixels inside the image: the centre tap's slot-3 weight is the bias
+        const float wv = !live ? 0.f : c < 3 ? w0[(co * 3 + c) * 9 + tap] : tap == 4 ? b0[co] : 0.f;
+        f0[(m * 64 + lane) * 8 + j] = (_Float16)wv;
       }
   for (int t = 0; t < Cfg::NT1; ++t)
     for (int m = 0; m < Cfg::KS1; ++m)
@@ -124,6 +126,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   constexpr int TASKS = V4 ? Cfg::INH * NG : Cfg::INH * Cfg::INW;
   constexpr int IT = (TASKS + 255) / 256;
   f32x4 v[IT][3];
+  bool okv[IT];  // the task's pixels lie inside the image (record slot 3 = 1: the folded bias)
   auto load_window = [&](const Tile& tl) {
     const float* xb = x + (int64_t)tl.img * 3 * plane;
     if constexpr (V4) {
@@ -134,6 +137,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
         const int r = t / NG, k = t - r * NG;
         const int iy = tl.Y0 - 1 + r, ix = A + 4 * k;
         const bool ok = t < TASKS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        okv[u] = ok;
         const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c)
@@ -146,6 +150,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
         const int r = t / Cfg::INW, c = t - r * Cfg::INW;
         const int iy = tl.Y0 - 1 + r, ix = tl.X0 - 1 + c;
         const bool ok = t < TASKS && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        okv[u] = ok;
         const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
         for (int ch = 0; ch < 3; ++ch) v[u][ch][0] = ok ? xb[ch * plane + o] : 0.f;
@@ -164,11 +169,11 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
           const int col = 4 * k - 2 + e;
           if (col < 0 || col >= Cfg::INW) continue;
           in[r * Cfg::INW + col] = h4{f16_rne(v[u][0][e] * scale), f16_rne(v[u][1][e] * scale),
-                                      f16_rne(v[u][2][e] * scale), (_Float16)0.f};
+                                      f16_rne(v[u][2][e] * scale), (_Float16)(okv[u] ? 1.f : 0.f)};
         }
       } else {
         in[t] = h4{f16_rne(v[u][0][0] * scale), f16_rne(v[u][1][0] * scale), f16_rne(v[u][2][0] * scale),
-                   (_Float16)0.f};
+                   (_Float16)(okv[u] ? 1.f : 0.f)};
       }
     }
   };
@@ -195,9 +200,6 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
       boff[m][u] = (set * 16 + (tap / 3) * Cfg::INW + tap % 3) * 8;
     }
   }
-  float bias0[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) bias0[q] = b0[4 * g + q];
   const int my_set = (4 * g) / Cfg::C0M, cbase = (4 * g) % Cfg::C0M;  // rows of D this lane holds
   unsigned char* l0w = l0 + ((cbase >> 3) * Cfg::L0H * 2 * Cfg::L0P) * 16 + (cbase & 7) * 2;
   // second-conv weights: k = tap*C0 + c; lane g of k-step m holds k = 32m + 8g .. +7
@@ -227,36 +229,44 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
     // workgroups whose first-conv window lies inside the image skip the per-pixel padding test
     const bool interior = tl.Y0 >= 0 && tl.X0 >= 0 && tl.Y0 + Cfg::L0H <= H && tl.X0 + Cfg::L0W <= W;
 
-    // ---- 2. first conv, 16 * PS pixels per MFMA group
+    // ---- 2. first conv, 16 * PS pixels per MFMA group (bias folded into the MFMA: record slot 3); interior tiles
+    // run a copy of the loop without the per-pixel padding test
     constexpr int P0V = Cfg::L0H * Cfg::INW;
     const unsigned char* inb = reinterpret_cast<const unsigned char*>(in);
-    for (int pt = wave; pt * 16 * PS < P0V; pt += 4) {
-      const int p0 = pt * 16 * PS + r16;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    auto conv1 = [&](auto interior_c) {
+      constexpr bool INTERIOR = decltype(interior_c)::value;
+      for (int pt = wave; pt * 16 * PS < P0V; pt += 4) {
+        const int p0 = pt * 16 * PS + r16;
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int m = 0; m < KS0; ++m) {
-        const h4 lo = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][0]);
-        const h4 hi = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][1]);
-        const h8 bf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[m], bf, acc, 0, 0, 0);
-      }
-      const int p = p0 + my_set * 16;
-      const int lr = p / Cfg::INW, lc = p - lr * Cfg::INW;
-      if (p >= P0V || lc >= Cfg::L0W) continue;
-      bool inside = true;
-      if (!interior) {
-        const int iy = tl.Y0 + lr, ix = tl.X0 + lc;
-        inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
-      }
-      h4 hv;
+        for (int m = 0; m < KS0; ++m) {
+          const h4 lo = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][0]);
+          const h4 hi = *reinterpret_cast<const h4*>(inb + p0 * 8 + boff[m][1]);
+          const h8 bf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[m], bf, acc, 0, 0, 0);
+        }
+        const int p = p0 + my_set * 16;
+        const int lr = p / Cfg::INW, lc = p - lr * Cfg::INW;
+        if (p >= P0V || lc >= Cfg::L0W) continue;
+        h4 hv;
+        if constexpr (INTERIOR) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float sv = silu_fast(acc[q] + bias0[q]);
-        hv[q] = f16_rne(inside ? sv : 0.f);
+          for (int q = 0; q < 4; ++q) hv[q] = f16_rne(silu_fast(acc[q]));
+        } else {
+          const int iy = tl.Y0 + lr, ix = tl.X0 + lc;
+          const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float sv = silu_fast(acc[q]);
+            hv[q] = f16_rne(inside ? sv : 0.f);
+          }
+        }
+        const int rec = lr * 2 * Cfg::L0P + (lc & 1) * Cfg::L0P + (lc >> 1);
+        *reinterpret_cast<h4*>(l0w + rec * 16) = hv;
       }
-      const int rec = lr * 2 * Cfg::L0P + (lc & 1) * Cfg::L0P + (lc >> 1);
-      *reinterpret_cast<h4*>(l0w + rec * 16) = hv;
-    }
+    };
+    if (interior) conv1(std::true_type{});
+    else conv1(std::false_type{});
     __syncthreads();
 
     // ---- 3. second conv: TH rows x TW cols, 16-pixel row segments
