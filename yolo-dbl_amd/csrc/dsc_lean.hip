@@ -333,6 +333,9 @@ static void lean_go(const ConvArgs<_Float16>& a, const float* dww, const float* 
   lean_go2<C, CO, K, S, TH, TW, NT, TG, false>(a, dww, dwb, dw_act, s);
 }
 
+constexpr int64_t LEAN_MAX_TILES_WIDE = 160;
+static int64_t lean_tiles8(const ConvArgs<_Float16>& a) { return (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 8); }
+
 // Shapes built (DBL-n / DBL-s neck and head, fp16): DSBottleneck's k3 / k7 DSConvs at 64 / 128 channels, the
 // stride-2 DSConvs 128 -> 128 / 256, and the Detect DWConv -> Conv1x1 pairs (c_in 64 / 128 / 256 -> 64).
 bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, int k, int st, int dil,
@@ -342,6 +345,12 @@ bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dw
   if (a.xcs % 8 || a.ycs % 4 || (a.res && a.rcs % 4) || a.KPAD != a.Cin) return false;
   const int c = a.Cin, co = a.Cout;
   if (a.t3w && co != 64) return false;
+  // 128+ input channels only while the map is small enough that the chunked kernel cannot fill the chip
+  // (<= 160 8x8 tiles: DBL-n's 20^2 maps at bs16).  On DBL-s bs64 (800 tiles at 40^2) and DBL-l 1280
+  // (400 tiles at 80^2) the lean kernel's 512-thread one-round-trip tiles lost to the chunked kernel:
+  // +43 / +35 ms over the bench's profile run (profiles/r03/r03rec_c{3,4}_*).  Must agree with
+  // ydbl.nn.modules.C3._cv3_fusable (the trailing GEMM exists only here).
+  if (c >= 128 && lean_tiles8(a) > LEAN_MAX_TILES_WIDE) return false;
   if (a.g2w) {  // DSC3k's last bottleneck k7 DSConv + its cv3 (ydbl.h: g2)
     if (st != 1 || k != 7 || c != co || a.g2xcs % 8 || a.g2ycs % 4) return false;
     if (c == 64) return lean_go<64, 64, 7, 1, 8, 8, 256, true>(a, dww, dwb, dw_act, s), true;

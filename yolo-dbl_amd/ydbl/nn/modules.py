@@ -549,7 +549,10 @@ class C3(nn.Module):
             return False
         dw, pw = last.cv2.dw, last.cv2.pw
         c3 = self.cv3.conv
-        return (c_ in (64, 128) and dw.kernel_size == (7, 7) and dw.stride == (1, 1) and dw.dilation == (1, 1)
+        # 128 channels only on small maps (csrc/dsc_lean.hip: LEAN_MAX_TILES_WIDE 8x8 tiles), where the lean kernel runs
+        small = x.n * -(-x.h // 8) * -(-x.w // 8) <= 160
+        return ((c_ == 64 or (c_ == 128 and small)) and dw.kernel_size == (7, 7) and dw.stride == (1, 1)
+                and dw.dilation == (1, 1)
                 and dw.bias is None and dw.in_channels == pw.out_channels == c_ and last.cv1.pw.out_channels == c_
                 and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.groups == 1
                 and c3.in_channels == 2 * c_ and c3.out_channels == c_ and isinstance(self.cv3.act, nn.SiLU))
