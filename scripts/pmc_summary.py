@@ -25,12 +25,12 @@ ROOT = Path(__file__).resolve().parent.parent
 FAMILIES = {  # family -> (kernel-name keys, FETCH_SIZE multiplier)
     "conv2d": (("conv_igemm_kernel", "conv3x3_tile_kernel", "conv_wsk_kernel", "conv3x3_halo_kernel",
                 "conv3x3_vw_kernel"), 2),
-    "dsconv": (("dsconv_kernel",), 2),
+    "dsconv": (("dsconv_kernel", "dsc_lean_kernel"), 2),
     "bottleneck": (("bneck_kernel",), 2),
     "stem2": (("stem2_kernel",), 2),
     "stem": (("stem_kernel",), 2),
     "depthwise": (("dwconv_lds_kernel", "dwconv_kernel", "dw_pair_kernel"), 2),
-    "hypergraph": (("hg_",), 2),
+    "hypergraph": (("hg_", "hg3_"), 2),
     "dysample": (("dysample_kernel",), 2),
     "decode": (("decode_kernel",), 1),
     "nms": (("nms_kernel",), 1),

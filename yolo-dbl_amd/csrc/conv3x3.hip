@@ -211,7 +211,9 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   // 49.6 us, 192->64 45.9 vs 28.0 us); 384->64 @40^2 also beats the wave-split-K kernel it used to
   // take (78.8 us).  (P >= 51200 already guarantees >= 400 8-row tiles.)
   (void)tiles8;
-  if (a.Ho % 16 == 0 && a.Cout > 32 && tiles16 >= 512) launch_halo<T, Q8, 1, 16>(a, s);
+  // Cout <= 32 (one 32-channel slice: the weights are as many bytes per chunk as the halo): 16-row tiles from
+  // 256 of them (DBL-n's 256->32 @80^2 at bs16, 400 tiles: 34.6 -> 31.8 us in graph, scripts/kbench.py)
+  if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256)) launch_halo<T, Q8, 1, 16>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);
   return true;
 }

@@ -175,6 +175,36 @@ class Plan:
         torch.cuda.synchronize(self.device)
         return [(w, a.elapsed_time(b)) for w, a, b in evs]
 
+    def run_graph_timed(self, reps: int = 8, iters: int = 3):
+        """Per-launch time as the kernels run inside the step's hipGraph: every launch captured `reps`
+        times back to back into a graph of its own, replayed `iters` times between a HIP event pair on
+        the replaying stream; min replay time / reps.  Unlike run_timed this carries no per-launch host
+        or event overhead, so it agrees with rocprofv3's kernel durations (bench.py's roofline)."""
+        out = []
+        for st in self.steps:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+                for _ in range(reps):
+                    rc = st.fn(*st.args, s)
+                    if rc:
+                        _lib.check(rc, st.what)
+            g.replay()
+            torch.cuda.synchronize(self.device)
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            best = float("inf")
+            for _ in range(iters):
+                torch.cuda._sleep(int(2e6))
+                a.record()
+                g.replay()
+                b.record()
+                torch.cuda.synchronize(self.device)
+                best = min(best, a.elapsed_time(b) / reps)
+            out.append((st.what, best))
+            del g
+        return out
+
 
 class GraphRunner:
     """Captures Plan.run into a hipGraph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it."""
