@@ -1,4 +1,4 @@
-"""Per-launch HIP-event profile of one compiled inference plan (forward + decode + NMS).
+"""Per-launch in-graph profile of one compiled inference plan (forward + decode + NMS).
 
     python scripts/layer_profile.py [--model n] [--batch 32] [--imgsz 640] [--fp32] [--top 40]
 
@@ -35,14 +35,14 @@ def main():
     s = m.session(a.batch, a.imgsz, a.imgsz, half=not a.fp32, conf=0.25, iou=0.7, use_graph=False)
     s.load(blob_images(a.batch, a.imgsz, seed=1234).cuda())
     el = 4 if a.fp32 else 2
-    best = None
-    for _ in range(5):
-        t = s.plan.run_timed()
-        best = t if best is None else [(w, min(x, y)) for (w, x), (_, y) in zip(best, t)]
+    best = s.plan.run_graph_timed()
     rows = []
     for i, (st, (what, ms)) in enumerate(zip(s.plan.steps, best)):
         kind = st.fn.__name__.replace("ydbl_", "")
         shape, gbs = "", ""
+        d0 = st.args[0] if st.args else None
+        if hasattr(d0, "x") and hasattr(d0, "y") and hasattr(d0.x, "c") and kind not in ("conv2d_nhwc", "dwconv2d_nhwc"):
+            shape = f"{d0.x.c}x{d0.x.h}x{d0.x.w}->{d0.y.c}x{d0.y.h}x{d0.y.w}"
         if kind in ("conv2d_nhwc", "dwconv2d_nhwc"):
             d = st.args[0]
             shape = f"{d.x.c}x{d.x.h}x{d.x.w}->{d.y.c}x{d.y.h}x{d.y.w} k{d.kh} s{d.stride} d{d.dil}"
@@ -54,7 +54,7 @@ def main():
                 gbs = f"{b / (ms * 1e-3) / 1e9:7.0f} GB/s"
         rows.append((i, kind, what, shape, ms * 1e3, gbs))
     total = sum(r[4] for r in rows)
-    print(f"total {total:.1f} us over {len(rows)} launches  ({a.batch * 1e6 / total:.0f} img/s eager-sum)")
+    print(f"total {total:.1f} us over {len(rows)} launches  ({a.batch * 1e6 / total:.0f} img/s in-graph sum)")
     by = {}
     for r in rows:
         by[r[1]] = by.get(r[1], 0) + r[4]
