@@ -68,6 +68,9 @@ def dsconv_traffic(step, elsize):
     if d.g2_w:  # trailing GEMM (C3's cv3): y stays on chip; the cv2 branch is read and cv3's output written
         byts += (_px(d.g2_x) * d.g2_x.c + _px(d.g2_y) * d.g2_y.c - _px(y) * y.c) * elsize
         flops += 2.0 * _px(d.g2_y) * d.g2_y.c * (y.c + d.g2_x.c)
+    if d.g0_w:  # leading 1x1 (C3's cv2 | cv1): its input read and both outputs written instead of x read
+        byts += (_px(d.g0_x) * d.g0_x.c + _px(d.g0_y) * d.g0_y.c - _px(x) * x.c) * elsize + d.g0_y.c * d.g0_x.c * elsize
+        flops += 2.0 * _px(d.g0_y) * d.g0_y.c * d.g0_x.c
     return byts, flops
 
 

@@ -132,6 +132,16 @@ typedef struct {
   const float* g2_b;
   ydbl_view g2_x, g2_y;
   int32_t g2_act;
+  /* optional leading 1x1 conv (C3's merged cv2 | cv1 ahead of its first DSBottleneck, block.py:259-273 for
+   * DSC3k block.py:1447-1503): g0_y[p] = g0_act(g0_w g0_x[p] + g0_b), all g0_y.c channels written, and this
+   * DSConv's x is the last x.c channels of g0_y, recomputed on the tile's halo from g0_x instead of read back
+   * (x must be exactly that channel slice of g0_y).  g0_w [g0_y.c][g0_x.c] in the view dtype (k contiguous),
+   * g0_b fp32.  Built for fp16, k 3 stride 1, g0_x.c == x.c == y.c == 64, g0_y.c == 128; g0_w == NULL
+   * disables it. */
+  const void* g0_w;
+  const float* g0_b;
+  ydbl_view g0_x, g0_y;
+  int32_t g0_act;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 

@@ -1054,6 +1054,7 @@ def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
     o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=c).eval()
     x = torch.randn(*shape)
     outs, nsteps = [], []
+    monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")  # the leading-1x1 fusion has its own test (below)
     for fuse in ("1", ""):
         if fuse:
             monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
@@ -1068,6 +1069,44 @@ def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
         pm.emit(plan, xv, yv)
         nsteps.append(len(plan.steps))
         assert any("+cv3" in st.what for st in plan.steps) == bool(fuse)
+        _run(plan)
+        outs.append(yv.nchw().float().cpu())
+    assert nsteps[0] == nsteps[1] - 1
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+    with torch.no_grad():
+        ref = o(x)
+    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("n,shape,sliced", [(2, (16, 64, 40, 40), False), (1, (3, 64, 13, 21), True),
+                                            (2, (2, 64, 9, 7), True)])
+def test_dsc3k_cv1_fused_bit_identical(n, shape, sliced, monkeypatch):
+    """DSC3k at c_ = 64: the merged cv2 | cv1 1x1 as the leading GEMM of the first bottleneck's k3 DSConv
+    (ydbl_dsconv_desc.g0: cv1's map recomputed on the tile halo, zero outside the image, both 1x1 outputs still
+    written) == the separate 1x1 + k3 DSConv launches, bit for bit; one launch fewer; close to the oracle."""
+    from oracle import model as om
+    from ydbl.nn import modules as M
+    from ydbl.utils.synthetic import trained_like_
+
+    c = 64
+    torch.manual_seed(n + shape[2])
+    o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=7).eval()
+    x = torch.randn(*shape)
+    outs, nsteps = [], []
+    for fuse in ("1", ""):
+        if fuse:
+            monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
+        else:
+            monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")
+        pm = M.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7)
+        pm.load_state_dict(o.state_dict())
+        plan = _plan(torch.float16)
+        xv = _tv_from_nchw(plan, x)
+        ybuf = plan.alloc(shape[0], shape[2], shape[3], c + (24 if sliced else 0))
+        yv = ybuf.cslice(8, c) if sliced else ybuf
+        pm.emit(plan, xv, yv)
+        nsteps.append(len(plan.steps))
+        assert any(st.what.startswith("Conv1x1x2+") for st in plan.steps) == bool(fuse)
         _run(plan)
         outs.append(yv.nchw().float().cpu())
     assert nsteps[0] == nsteps[1] - 1

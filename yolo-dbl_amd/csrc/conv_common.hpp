@@ -30,6 +30,10 @@ struct ConvArgs {
   const T* g2w; const float* g2b;
   const T* g2x; int g2xcs;
   T* g2y; int g2ycs; int g2act;
+  // optional leading 1x1 (dsc_lean.hip, C3's merged cv2|cv1): g0y = g0act(g0w g0x + g0b), x = g0y's last Cin channels
+  const T* g0w; const float* g0b;
+  const T* g0x; int g0xcs;
+  T* g0y; int g0ycs; int g0act;
 };
 
 // ---- in-launch hand-off of per-workgroup partials (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1

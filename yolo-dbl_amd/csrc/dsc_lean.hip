@@ -25,7 +25,7 @@ namespace ydbl {
 
 __device__ __forceinline__ int lean_bswz(int row, int kv) { return row * 4 + (kv ^ (((row >> 2) & 1) << 1)); }
 
-template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false, bool TAIL = false>
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false, bool TAIL = false, bool PRE = false>
 __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, const float* __restrict__ dww,
                                                           const float* __restrict__ dwb, int dw_act, int tiles_x,
                                                           int tiles_y, int ntiles) {
@@ -59,10 +59,15 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
   constexpr int NKS2 = TG ? 2 * CO / 32 : 0;
   static_assert(!TG || (C == CO && NKS2 * NPX * 4 * 16 <= IH * IWP * NQ * 8), "trailing GEMM layout");
   constexpr int X2V = TG ? NPX * CO / 8 : 1, X2IT = (X2V + NT - 1) / NT;
+  // PRE: leading 1x1 g0y = act(W0 g0x + b0) (2C outputs: C3's cv2 | cv1) over the whole halo, its last C channels
+  // are this DSConv's input; B tile [2 k-steps][halo pixel, padded to 16][slot], one 16-channel tile pair per wave
+  static_assert(!PRE || (C == 64 && CO == 64 && S == 1 && !TG && !TAIL && WAVES == 4), "leading 1x1 layout");
+  constexpr int PNP = PRE ? (IH * IW + 15) / 16 * 16 : 16, PNT = PNP / 16;
   __shared__ h4 s_x[IH * IWP * NQ];                  // fp16 halo, [row][col][quad]
   __shared__ f32x4 s_w[TAPV];                        // fp32 taps (rounded to fp16), [tap][quad]
   __shared__ h8 s_b[NKS * NPX * 4];                  // pointwise B tile, [k-step][pixel][slot]
   h8* s_g = reinterpret_cast<h8*>(s_x);              // TG: trailing GEMM B tile (after the depthwise phase)
+  __shared__ h8 s_p[PRE ? 2 * PNP * 4 : 1];          // PRE: the leading 1x1's B tile (g0x halo)
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -89,6 +94,8 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
     return tl;
   };
   h8 xr[HIT];
+  const T* xsrc = PRE ? p.g0x : p.x;
+  const int xscs = PRE ? p.g0xcs : p.xcs;
   auto load_halo = [&](const Tile& tl) {
 #pragma unroll
     for (int it = 0; it < HIT; ++it) {
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
       const int hy = px / IW, hx = px - hy * IW;
       const int iy = tl.iy0 + hy, ix = tl.ix0 + hx;
       const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-      xr[it] = vload_sel(p.x + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.xcs + cv * 8, p.x, ok);
+      xr[it] = vload_sel(xsrc + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * xscs + cv * 8, xsrc, ok);
     }
   };
 
@@ -118,6 +125,17 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
     const int row = (cg * TN + i) * 16 + r16;  // A rows: output channel of this lane
 #pragma unroll
     for (int m = 0; m < NKS; ++m) af[i][m] = vload(p.w + (int64_t)row * p.KPAD + m * 32 + g * 8);
+  }
+  h8 a0[2][2];  // PRE: this wave's two 16-channel tiles of W0, both k-steps
+  float b0v[2][4];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = (wave * 2 + i) * 16 + r16;
+#pragma unroll
+      for (int m = 0; m < 2; ++m) a0[i][m] = vload(p.g0w + (int64_t)row * C + m * 32 + g * 8);
+      load_f<4>(p.g0b + (wave * 2 + i) * 16 + 4 * g, b0v[i]);
+    }
   }
 #pragma unroll
   for (int it = 0; it < TIT; ++it)
@@ -157,11 +175,52 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
       const int i = tid + it * NT;
       if (i < HV) {
         const int cv = i % CV, px = i / CV;
-        const int hy = px / IW, hx = px - hy * IW;
-        *reinterpret_cast<h8*>(&s_x[(hy * IWP + hx) * NQ + cv * 2]) = xr[it];
+        if constexpr (PRE) {
+          s_p[(cv >> 2) * PNP * 4 + lean_bswz(px, cv & 3)] = xr[it];
+        } else {
+          const int hy = px / IW, hx = px - hy * IW;
+          *reinterpret_cast<h8*>(&s_x[(hy * IWP + hx) * NQ + cv * 2]) = xr[it];
+        }
+      }
+    }
+    if constexpr (PRE) {  // the pad pixels of the last 16-pixel tile: finite zeros (never stored)
+      for (int i = tid; i < (PNP - IH * IW) * CV; i += NT) {
+        const int cv = i % CV, px = IH * IW + i / CV;
+        s_p[(cv >> 2) * PNP * 4 + lean_bswz(px, cv & 3)] = h8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
     __syncthreads();
+    if constexpr (PRE) {
+      // ---- 1b. leading 1x1 over the halo on MFMA (k-steps in channel order, epilogue as conv_epilogue's):
+      // every output pixel's 2C values -> g0y; the last C channels (zero outside the image: the depthwise
+      // padding) -> the fp16 halo in LDS, exactly what the unfused DSConv would read back
+      for (int j = 0; j < PNT; ++j) {
+        f32x4 pa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          const h8 bf = s_p[m * PNP * 4 + lean_bswz(j * 16 + r16, g)];
+#pragma unroll
+          for (int i = 0; i < 2; ++i) pa[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i][m], bf, pa[i], 0, 0, 0);
+        }
+        const int px = j * 16 + r16;
+        const int hy = px / IW, hx = px - hy * IW;
+        const int iy = tl.iy0 + hy, ix = tl.ix0 + hx;
+        const bool live = px < IH * IW;
+        const bool inimg = live && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        const bool outpx = inimg && hy >= p.PAD && hy < p.PAD + TH && hx >= p.PAD && hx < p.PAD + TW;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int c = (wave * 2 + i) * 16 + 4 * g;
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(pa[i][q] + b0v[i][q], p.g0act);
+          const h4 o = to_h4_rne(v);
+          if (outpx) *reinterpret_cast<h4*>(p.g0y + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.g0ycs + c) = o;
+          if (wave >= 2 && live) s_x[(hy * IWP + hx) * NQ + (c - C) / 4] = inimg ? o : h4{0, 0, 0, 0};
+        }
+      }
+      __syncthreads();
+    }
 
     // ---- 2. depthwise: task = (quad q, output row r, segment sg), quad fastest
     {
@@ -313,13 +372,13 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
   }
 }
 
-template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool TAIL>
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool TAIL, bool PRE = false>
 static void lean_go2(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, TW), tiles_y = (int)cdiv(a.Ho, TH);
   const int ntiles = a.N * tiles_y * tiles_x;
   // (measured and not kept: a persistent walk with the next tile's halo prefetched -- 2-3 workgroups per CU,
   // VGPR-bound, slower or even on every DBL-n shape but the 80^2 stride-2 one, which the chunked kernel takes)
-  dsc_lean_kernel<C, CO, K, S, TH, TW, NT, TG, TAIL><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x,
+  dsc_lean_kernel<C, CO, K, S, TH, TW, NT, TG, TAIL, PRE><<<(unsigned)ntiles, NT, 0, s>>>(a, dww, dwb, dw_act, tiles_x,
                                                                                      tiles_y, ntiles);
 }
 
@@ -329,6 +388,9 @@ template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false>
 static void lean_go(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, hipStream_t s) {
   if constexpr (CO == 64 && !TG) {
     if (a.t3w) return lean_go2<C, CO, K, S, TH, TW, NT, TG, true>(a, dww, dwb, dw_act, s);
+  }
+  if constexpr (C == 64 && CO == 64 && K == 3 && S == 1 && !TG) {
+    if (a.g0w) return lean_go2<C, CO, K, S, TH, TW, NT, TG, false, true>(a, dww, dwb, dw_act, s);
   }
   lean_go2<C, CO, K, S, TH, TW, NT, TG, false>(a, dww, dwb, dw_act, s);
 }
@@ -345,6 +407,7 @@ bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dw
   if (a.xcs % 8 || a.ycs % 4 || (a.res && a.rcs % 4) || a.KPAD != a.Cin) return false;
   const int c = a.Cin, co = a.Cout;
   if (a.t3w && co != 64) return false;
+  if (a.g0w && !(st == 1 && k == 3 && c == 64 && co == 64)) return false;  // the leading 1x1 (ydbl.h g0)
   // 128+ input channels only while the map is small enough that the chunked kernel cannot fill the chip
   // (<= 160 8x8 tiles: DBL-n's 20^2 maps at bs16).  On DBL-s bs64 (800 tiles at 40^2) and DBL-l 1280
   // (400 tiles at 80^2) the lean kernel's 512-thread one-round-trip tiles lost to the chunked kernel:

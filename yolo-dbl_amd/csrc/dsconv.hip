@@ -281,6 +281,17 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
     }
     return fail(YDBL_EINVAL, "dsconv: the trailing GEMM (g2) needs fp16, k 7 stride 1, C 64 or 128 (lean kernel)");
   }
+  if (d->g0_w) {  // leading 1x1: only the lean kernel has it (ydbl.h: fp16, k 3 s 1, C 64, g0_y 128)
+    a.g0w = reinterpret_cast<const T*>(d->g0_w); a.g0b = d->g0_b;
+    a.g0x = reinterpret_cast<const T*>(d->g0_x.ptr); a.g0xcs = d->g0_x.cs;
+    a.g0y = reinterpret_cast<T*>(d->g0_y.ptr); a.g0ycs = d->g0_y.cs; a.g0act = d->g0_act;
+    if constexpr (sizeof(T) == 2) {
+      if (d->k == 3 && d->stride == 1 && d->dil == 1 &&
+          try_dsc_lean(a, d->dw_w, d->dw_bias, d->dw_act, 3, 1, 1, s))
+        return check_launch("ydbl_dsconv_nhwc");
+    }
+    return fail(YDBL_EINVAL, "dsconv: the leading 1x1 (g0) needs fp16, k 3 stride 1, C 64 (lean kernel)");
+  }
   if (d->k == 3 && d->stride == 1 && d->dil == 1) return launch_ds<T, 3, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
   if (d->k == 3 && d->stride == 2 && d->dil == 1) return launch_ds<T, 3, 2, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
   if (d->k == 5 && d->stride == 1 && d->dil == 1) return launch_ds<T, 5, 1, 1>(a, d->dw_w, d->dw_bias, d->dw_act, s);
@@ -316,6 +327,17 @@ extern "C" int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream) {
         d->g2_y.dtype != d->y.dtype || d->g2_y.cs % 4 || d->g2_x.n != d->y.n || d->g2_x.h != d->y.h ||
         d->g2_x.w != d->y.w || d->g2_y.n != d->y.n || d->g2_y.h != d->y.h || d->g2_y.w != d->y.w)
       return fail(YDBL_EINVAL, "dsconv: g2 needs g2_x/g2_y of y's shape and dtype, x.c == y.c, no class tail");
+  }
+  if (d->g0_w) {
+    const int es = d->y.dtype == YDBL_F16 ? 2 : 4;
+    if (!d->g0_b || check_view(&d->g0_x, "dsconv.g0_x", true) || check_view(&d->g0_y, "dsconv.g0_y", false) ||
+        d->g0_x.c != d->x.c || d->g0_y.c != 2 * d->x.c || d->x.c != d->y.c || d->g2_w || d->tail_w ||
+        d->g0_x.dtype != d->x.dtype || d->g0_y.dtype != d->x.dtype || d->g0_y.cs % 4 || d->g0_x.cs % 8 ||
+        d->res_mode != YDBL_RES_NONE || d->g0_x.n != d->x.n || d->g0_x.h != d->x.h || d->g0_x.w != d->x.w ||
+        d->g0_y.n != d->x.n || d->g0_y.h != d->x.h || d->g0_y.w != d->x.w || d->x.cs != d->g0_y.cs ||
+        (const char*)d->x.ptr != (const char*)d->g0_y.ptr + (int64_t)d->x.c * es)
+      return fail(YDBL_EINVAL, "dsconv: g0 needs g0_x [n,h,w,x.c], g0_y [n,h,w,2 x.c] whose last x.c channels are x, "
+                               "x.c == y.c, no residual / tail / g2");
   }
   if (d->tail_w) {
     if (!d->tail_b || d->tail_n < 1 || d->tail_n > 4 || d->y.c != 64 || d->res_mode != YDBL_RES_NONE ||

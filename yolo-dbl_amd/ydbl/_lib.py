@@ -46,7 +46,8 @@ class DsConvDesc(C.Structure):
                 ("dil", C.c_int32), ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32),
                 ("dw_bias", C.c_void_p), ("dw_act", C.c_int32), ("tail_w", C.c_void_p), ("tail_b", C.c_void_p),
                 ("tail_y", View), ("tail_n", C.c_int32), ("g2_w", C.c_void_p), ("g2_b", C.c_void_p),
-                ("g2_x", View), ("g2_y", View), ("g2_act", C.c_int32)]
+                ("g2_x", View), ("g2_y", View), ("g2_act", C.c_int32), ("g0_w", C.c_void_p), ("g0_b", C.c_void_p),
+                ("g0_x", View), ("g0_y", View), ("g0_act", C.c_int32)]
 
 
 class HgDesc(C.Structure):

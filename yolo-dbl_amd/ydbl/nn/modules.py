@@ -163,12 +163,14 @@ def fused_dsconv_ok(dw: nn.Conv2d, x: TV, dtype) -> bool:
 def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Tensor, b_pw: torch.Tensor,
                 act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv",
                 w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE,
-                tail: tuple | None = None, g2: tuple | None = None) -> TV:
+                tail: tuple | None = None, g2: tuple | None = None, g0: tuple | None = None) -> TV:
     """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA.
     w_dw / b_dw / dw_act: folded DWConv weights, bias and activation (Detect's DWConv -> Conv1x1 pair).
     tail = (w [n, co], b [n], out view): a trailing 1x1 conv with n <= 4 outputs in the same launch.
     g2 = (w [co2, co + c2] fp32, b [co2], x2 view, y2 view, act): a trailing GEMM over [y ; x2] into y2 (C3's
-    cv3 after the last bottleneck); y itself is then not stored (include/ydbl.h, ydbl_dsconv_desc.g2)."""
+    cv3 after the last bottleneck); y itself is then not stored (include/ydbl.h, ydbl_dsconv_desc.g2).
+    g0 = (w [c0y, c0x] fp32, b [c0y], x0 view, y0 view, act): a leading 1x1 y0 = act(w x0 + b) written by the same
+    launch, x being y0's last x.c channels, recomputed on the tile halo (C3's merged cv2 | cv1, ydbl_dsconv_desc.g0)."""
     k, st, p, d = dw.kernel_size[0], dw.stride[0], dw.padding[0], dw.dilation[0]
     c = x.c
     co = w_pw.shape[0]
@@ -193,10 +195,17 @@ def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Te
         g2w, g2b = plan.const(g2[0].float().to(plan.dtype).contiguous()), plan.const(g2[1].float().contiguous())
         g2_args = (g2w.data_ptr(), g2b.data_ptr(), g2[2].struct(), g2[3].struct(), int(g2[4]))
         what += "+cv3"
+    g0w = g0b = None
+    g0_args = (None, None, _null_view(), _null_view(), 0)
+    if g0 is not None:
+        g0w, g0b = plan.const(g0[0].float().to(plan.dtype).contiguous()), plan.const(g0[1].float().contiguous())
+        g0_args = (g0w.data_ptr(), g0b.data_ptr(), g0[2].struct(), g0[3].struct(), int(g0[4]))
+        what = "Conv1x1x2+" + what
     desc = _lib.DsConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(),
                            dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode,
-                           dwb.data_ptr() if dwb is not None else None, dw_act, *tail_args, *g2_args)
-    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}", keep=[dww, pww, bd, dwb, tw, tb, g2w, g2b, desc])
+                           dwb.data_ptr() if dwb is not None else None, dw_act, *tail_args, *g2_args, *g0_args)
+    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}",
+                keep=[dww, pww, bd, dwb, tw, tb, g2w, g2b, g0w, g0b, desc])
     return y
 
 
@@ -524,11 +533,20 @@ class C3(nn.Module):
         if mergeable([self.cv2, self.cv1]) and not os.environ.get("YDBL_NO_MERGE"):
             # cv2 and cv1 both read x: one launch into [m slot | cv2 | cv1] (cv3 reads the first 2c_)
             buf = plan.alloc(x.n, x.h, x.w, 3 * c_)
-            emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
             if self._cv3_fusable(plan, x):
-                # DSC3k: cv3 rides in the last DSBottleneck's k7 DSConv (its output never leaves the CU)
-                t = emit_seq(plan, list(self.m)[:-1], buf.cslice(2 * c_, c_)) if len(self.m) > 1 else buf.cslice(2 * c_, c_)
-                return self.m[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out))
+                # DSC3k: cv3 rides in the last DSBottleneck's k7 DSConv (its output never leaves the CU), and
+                # cv2 | cv1 in the first one's k3 DSConv where the lean kernel takes it (cv1's map recomputed on
+                # the halo; both outputs still written: cv3 and the first residual read them)
+                pre = (self.cv2, self.cv1, x, buf.cslice(c_, 2 * c_)) if self._cv1_fusable(plan, x) else None
+                if pre is None:
+                    emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
+                mods = list(self.m)
+                t = buf.cslice(2 * c_, c_)
+                for i, m in enumerate(mods[:-1]):
+                    t = m.emit(plan, t, pre=pre if i == 0 else None)
+                return mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
+                                     pre=pre if len(mods) == 1 else None)
+            emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
             emit_seq(plan, self.m, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
             return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
         buf = plan.alloc(x.n, x.h, x.w, 2 * c_)
@@ -537,6 +555,21 @@ class C3(nn.Module):
         self.cv2.emit(plan, x, buf.cslice(c_, c_))
         return self.cv3.emit(plan, buf, out)
 
+
+    def _cv1_fusable(self, plan, x) -> bool:
+        """cv2 | cv1 (merged 1x1, x.c -> 2 c_) can lead the first DSBottleneck's k3 DSConv in one launch
+        (dsc_lean.hip PRE, ydbl_dsconv_desc.g0): fp16, x.c == c_ == 64, SiLU 1x1s, that DSConv k3 stride 1 with
+        no depthwise bias, the lean kernel enabled."""
+        if (plan.dtype != torch.float16 or os.environ.get("YDBL_NO_CV1_FUSE") or os.environ.get("YDBL_DS_LEAN") == "0"
+                or not len(self.m) or not isinstance(self.m[0], DSBottleneck)):
+            return False
+        c_ = self.cv1.conv.out_channels
+        first = self.m[0].cv1
+        dw = first.dw
+        return (c_ == 64 and x.c == 64 and x.cs % 8 == 0 and self.cv1.conv.kernel_size == (1, 1)
+                and self.cv1.conv.stride == (1, 1) and isinstance(self.cv1.act, nn.SiLU)
+                and dw.kernel_size == (3, 3) and dw.stride == (1, 1) and dw.dilation == (1, 1) and dw.padding == (1, 1)
+                and dw.bias is None and dw.in_channels == c_ and first.pw.out_channels == c_)
 
     def _cv3_fusable(self, plan, x) -> bool:
         """cv3 can run as the trailing GEMM of the last bottleneck's k7 DSConv (dsc_lean.hip, ydbl_dsconv_desc.g2):
@@ -599,21 +632,31 @@ class DSBottleneck(nn.Module):
         self.cv2 = DSConv(c_, c2, k2, s=1, p=None, d=d2)
         self.add = shortcut and c1 == c2
 
-    def emit(self, plan, x, out=None, cv3=None):
+    def emit(self, plan, x, out=None, cv3=None, pre=None):
         """cv3 = (C3's cv3 Conv, its second input view (the cv2 branch), its output view or None): the DSC3k's
-        cv3 as the trailing GEMM of this bottleneck's k7 DSConv; returns cv3's output then."""
+        cv3 as the trailing GEMM of this bottleneck's k7 DSConv; returns cv3's output then.
+        pre = (C3's cv2, cv1, their input, their [cv2 | cv1] output view whose last c_ channels are x): the merged
+        1x1 as the leading GEMM of this bottleneck's k3 DSConv (C3._cv1_fusable)."""
         y = out if out is not None else plan.alloc(x.n, x.h, x.w, self.cv2.pw.out_channels)
+        if pre is not None:
+            c2m, c1m, x0, y0 = pre
+            (w2, b2), (w1, b1) = c2m.folded(), c1m.folded()
+            g0 = (torch.cat([w2, w1], 0).reshape(y0.c, x0.c), torch.cat([b2, b1], 0), x0, y0, _act_code(c1m.act))
+            wp, bp = fold_bn(self.cv1.pw.weight, self.cv1.pw.bias, self.cv1.bn)
+            t = emit_dsconv(plan, self.cv1.dw, x, None, wp, bp, _lib.ACT_SILU, g0=g0)
+        else:
+            t = None
         if cv3 is not None:
             conv3, x2, o3 = cv3
             o3 = o3 if o3 is not None else plan.alloc(x.n, x.h, x.w, conv3.conv.out_channels)
-            t = self.cv1.emit(plan, x)
+            t = t if t is not None else self.cv1.emit(plan, x)
             w, b = fold_bn(self.cv2.pw.weight, self.cv2.pw.bias, self.cv2.bn)
             w3, b3 = conv3.folded()
             emit_dsconv(plan, self.cv2.dw, t, y, w, b, _lib.ACT_SILU, x if self.add else None,
                         _lib.RES_ADD if self.add else _lib.RES_NONE,
                         g2=(w3.reshape(w3.shape[0], -1), b3, x2, o3, _act_code(conv3.act)))
             return o3
-        t = self.cv1.emit(plan, x)
+        t = t if t is not None else self.cv1.emit(plan, x)
         return self.cv2.emit(plan, t, y, res=x if self.add else None,
                              res_mode=_lib.RES_ADD if self.add else _lib.RES_NONE)
 
