@@ -126,15 +126,18 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
 #pragma unroll
     for (int m = 0; m < NKS; ++m) af[i][m] = vload(p.w + (int64_t)row * p.KPAD + m * 32 + g * 8);
   }
-  h8 a0[2][2];  // PRE: this wave's two 16-channel tiles of W0, both k-steps
+  // PRE: tile i = 0 of this wave = 16 channels of the cv1 half (C + 16 wave.., over the whole halo, before the
+  // depthwise), i = 1 = 16 channels of the cv2 half (16 wave.., over the output pixels only, after the pointwise)
+  h8 a0[2][2];
   float b0v[2][4];
   if constexpr (PRE) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int row = (wave * 2 + i) * 16 + r16;
+      const int ct = i == 0 ? C / 16 + wave : wave;
+      const int row = ct * 16 + r16;
 #pragma unroll
       for (int m = 0; m < 2; ++m) a0[i][m] = vload(p.g0w + (int64_t)row * C + m * 32 + g * 8);
-      load_f<4>(p.g0b + (wave * 2 + i) * 16 + 4 * g, b0v[i]);
+      load_f<4>(p.g0b + ct * 16 + 4 * g, b0v[i]);
     }
   }
 #pragma unroll
@@ -194,30 +197,25 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
       // ---- 1b. leading 1x1 over the halo on MFMA (k-steps in channel order, epilogue as conv_epilogue's):
       // every output pixel's 2C values -> g0y; the last C channels (zero outside the image: the depthwise
       // padding) -> the fp16 halo in LDS, exactly what the unfused DSConv would read back
+      const int c = C + wave * 16 + 4 * g;
+#pragma unroll
       for (int j = 0; j < PNT; ++j) {
-        f32x4 pa[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+        f32x4 pa = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-          const h8 bf = s_p[m * PNP * 4 + lean_bswz(j * 16 + r16, g)];
-#pragma unroll
-          for (int i = 0; i < 2; ++i) pa[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[i][m], bf, pa[i], 0, 0, 0);
-        }
+        for (int m = 0; m < 2; ++m)
+          pa = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[0][m], s_p[m * PNP * 4 + lean_bswz(j * 16 + r16, g)], pa, 0, 0, 0);
         const int px = j * 16 + r16;
         const int hy = px / IW, hx = px - hy * IW;
         const int iy = tl.iy0 + hy, ix = tl.ix0 + hx;
         const bool live = px < IH * IW;
         const bool inimg = live && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         const bool outpx = inimg && hy >= p.PAD && hy < p.PAD + TH && hx >= p.PAD && hx < p.PAD + TW;
+        float v[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int c = (wave * 2 + i) * 16 + 4 * g;
-          float v[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(pa[i][q] + b0v[i][q], p.g0act);
-          const h4 o = to_h4_rne(v);
-          if (outpx) *reinterpret_cast<h4*>(p.g0y + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.g0ycs + c) = o;
-          if (wave >= 2 && live) s_x[(hy * IWP + hx) * NQ + (c - C) / 4] = inimg ? o : h4{0, 0, 0, 0};
-        }
+        for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(pa[q] + b0v[0][q], p.g0act);
+        const h4 o = to_h4_rne(v);
+        if (outpx) *reinterpret_cast<h4*>(p.g0y + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.g0ycs + c) = o;
+        if (live) s_x[(hy * IWP + hx) * NQ + (c - C) / 4] = inimg ? o : h4{0, 0, 0, 0};
       }
       __syncthreads();
     }
@@ -315,6 +313,26 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
 #pragma unroll
             for (int q = 0; q < 4; ++q) ys[i][j][q] = round_to<T>(v[q]);
           }
+        }
+      }
+    }
+    if constexpr (PRE) {
+      // ---- 3b. the cv2 half of the leading 1x1 over the output pixels (s_p is read-only since the first barrier)
+      const int c = wave * 16 + 4 * g;
+#pragma unroll
+      for (int j = 0; j < NTP; ++j) {
+        const int op = j * 16 + r16;
+        const int hpx = (op / TW + p.PAD) * IW + op % TW + p.PAD;
+        f32x4 pa = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          pa = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[1][m], s_p[m * PNP * 4 + lean_bswz(hpx, g)], pa, 0, 0, 0);
+        const int oy = tl.oy0 + op / TW, ox = tl.ox0 + op % TW;
+        if (oy < p.Ho && ox < p.Wo) {
+          float v[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(pa[q] + b0v[1][q], p.g0act);
+          store_f<4>(p.g0y + (((int64_t)tl.b * p.Ho + oy) * p.Wo + ox) * p.g0ycs + c, v);
         }
       }
     }
