@@ -528,9 +528,16 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // Shallow K (<= 128) on large maps: 2048 (8 per CU; each tile is a short k-loop, so more workgroups
   // hide each other's load latency: 64->128 @80^2 bs32 35.3 -> 28.1 us, 64->64 17.5 -> 16.4,
   // 128->64 22.2 -> 21.2).
+  // (bs16 sub-batch graphs, scripts/kbench.py: for K 128, 2048 only above 131072 pixels -- 128->64 1x1 @80^2
+  // 12.6 -> 11.3 us at 1024; K 64 keeps 2048 there, 64->128 @80^2 14.4 vs 15.6 us -- and 64x64 tiles for the
+  // deep-K (>= 512) 3x3 convs with >= 16384 output pixels: 64->64 s2 @80^2 14.6 -> 13.1 us; DBL-n bs32 on two
+  // streams 16.20 -> 16.30 k img/s over three pairs with the halo kernel's n2_below 512, DBL-s bs64 even)
   static const char* ov = getenv("YDBL_IGEMM_WANT");  // A/B knob for the benches
+  static const bool r2 = getenv("YDBL_IGEMM_R2") == nullptr;  // A/B knob (read once per process): round-2 rule
+  const int64_t big = r2 ? 131072 : 65536;
   const int64_t want = ov && *ov ? atoi(ov)
-                                 : (a.Cout <= 128 && a.P <= 65536 ? 512 : (a.K <= 128 && a.P > 65536 ? 2048 : 1024));
+                                 : (a.Cout <= 128 && a.P <= 65536 ? 512
+                                    : (a.K <= 128 && a.P > (a.K <= 64 ? 65536 : big) ? 2048 : 1024));
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   if (a.Cout <= 16) {
     if (blocks(256, 16) >= want) return launch_igemm<T, Q8, 256, 16, 4, 1>(a, pointwise, s);
@@ -544,7 +551,8 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   }
   if (a.Cout <= 64) {
     if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
-    if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
+    if (blocks(64, 64) >= want || (r2 && !pointwise && a.K >= 512 && a.P >= 16384))
+      return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
     return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
   }
   // Cout > 64: 64-wide column blocks (each workgroup stages half the weight rows; the input tile is read

@@ -162,7 +162,8 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   // most CUs with one workgroup; 32-channel slices double the grid (conv_bench.py bs16: 384->64 @40^2
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
   static const char* ev = getenv("YDBL_HALO_N2");  // A/B knob (read once per process)
-  const int64_t n2_below = ev && *ev ? atoll(ev) : 400;
+  // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench)
+  const int64_t n2_below = ev && *ev ? atoll(ev) : 512;
   if (a.Cout <= 32) {
     conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
