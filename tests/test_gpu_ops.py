@@ -1116,6 +1116,36 @@ def test_dsc3k_cv1_fused_bit_identical(n, shape, sliced, monkeypatch):
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
 
 
+def test_dsconv_g0_rejects_bad_descriptors():
+    """ydbl_dsconv_nhwc with a leading 1x1 (g0) refuses, before launching anything, descriptors whose x is not
+    the last x.c channels of g0_y, whose channel counts are not (64 -> 128, x.c 64), or that add a residual."""
+    import ctypes
+
+    from ydbl import _lib
+
+    plan = _plan(torch.float16)
+    n, h, w = 1, 8, 8
+    x0 = plan.alloc(n, h, w, 64)
+    buf = plan.alloc(n, h, w, 192)
+    y0, x, y = buf.cslice(64, 128), buf.cslice(128, 64), plan.alloc(n, h, w, 64)
+    dww = torch.zeros(9 * 64, device=DEV)
+    pww = torch.zeros(64 * 64, dtype=torch.float16, device=DEV)
+    bias = torch.zeros(128, device=DEV)
+    w0 = torch.zeros(128 * 64, dtype=torch.float16, device=DEV)
+    nv = _lib.View(None, 0, 0, 0, 0, 0, 0)
+
+    def desc(xv, y0v, res=None):
+        return _lib.DsConvDesc(xv.struct(), y.struct(), res.struct() if res is not None else nv, dww.data_ptr(),
+                               pww.data_ptr(), bias.data_ptr(), 3, 1, 1, 1, 64, _lib.ACT_SILU,
+                               _lib.RES_ADD if res is not None else _lib.RES_NONE, None, 0, None, None, nv, 0,
+                               None, None, nv, nv, 0, w0.data_ptr(), bias.data_ptr(), x0.struct(), y0v.struct(),
+                               _lib.ACT_SILU)
+    for d in (desc(buf.cslice(64, 64), y0),        # x is the first half of g0_y, not its last channels
+              desc(x, buf.cslice(64, 96)),          # g0_y.c != 2 x.c
+              desc(x, y0, res=y)):                  # no residual with g0
+        assert _lib.lib.ydbl_dsconv_nhwc(ctypes.byref(d), None) != 0
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("c,shape,spread,fullpad", [(128, (16, 128, 40, 40), 0.01, False), (256, (4, 256, 20, 20), 0.01, True),
                                                     (64, (2, 64, 13, 17), 0.3, True), (128, (3, 128, 9, 40), 1.0, False)])
