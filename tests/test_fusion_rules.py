@@ -1,0 +1,48 @@
+"""Host-side fusion rules of the plan builder (no GPU): which DSC3k blocks take the leading / trailing GEMMs.
+
+C3._cv1_fusable must agree with the lean DSConv kernel's g0 instance (csrc/dsc_lean.hip: fp16, c_ = x.c = 64,
+k3 stride 1) and C3._cv3_fusable with its g2 instances (k7, c_ 64 or 128 on small maps); a mismatch would make
+ydbl_dsconv_nhwc refuse the descriptor at plan build time on the GPU.
+"""
+from types import SimpleNamespace as NS
+
+import torch
+
+from ydbl.nn import modules as M
+
+
+def _x(n, c, h=40, w=40, cs=None):
+    return NS(n=n, c=c, h=h, w=w, cs=cs if cs is not None else c)
+
+
+def test_cv1_fusable_dbl_n_shape(monkeypatch):
+    monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
+    monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
+    m = M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=7)
+    plan = NS(dtype=torch.float16)
+    assert m._cv1_fusable(plan, _x(16, 64))
+    assert m._cv3_fusable(plan, _x(16, 64))
+    assert not m._cv1_fusable(NS(dtype=torch.float32), _x(16, 64))  # fp16 only
+    assert not m._cv1_fusable(plan, _x(16, 64, cs=68))  # 16-byte pixel vectors
+    monkeypatch.setenv("YDBL_DS_LEAN", "0")  # the chunked kernel has no leading GEMM
+    assert not m._cv1_fusable(plan, _x(16, 64))
+    monkeypatch.delenv("YDBL_DS_LEAN")
+    monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")
+    assert not m._cv1_fusable(plan, _x(16, 64))
+
+
+def test_cv1_fusable_only_at_64_channels_and_k3(monkeypatch):
+    monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
+    monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
+    plan = NS(dtype=torch.float16)
+    assert not M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)._cv1_fusable(plan, _x(16, 128, 20, 20))
+    assert not M.DSC3k(64, 64, 2, True, e=1.0, k1=5, k2=7)._cv1_fusable(plan, _x(16, 64))
+    # plain C3 (Bottleneck m) never takes it
+    assert not M.C3(64, 64, 1)._cv1_fusable(plan, _x(16, 64))
+
+
+def test_cv3_fusable_small_map_rule_for_128_channels():
+    plan = NS(dtype=torch.float16)
+    m = M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)
+    assert m._cv3_fusable(plan, _x(16, 128, 20, 20))      # 16 * 3 * 3 = 144 8x8 tiles <= 160
+    assert not m._cv3_fusable(plan, _x(64, 128, 40, 40))  # DBL-s bs64: 1600 tiles -> chunked kernel
