@@ -4,7 +4,7 @@ Default workload = BASELINE.json configs[1]: YOLO-DBL-n, 640x640, bs=32 per GPU,
 fp16, predict settings (conf 0.25, iou 0.7, max_det 300), synthetic blob images
 already resident in HBM, trained-like synthetic weights (tests/golden fixture).
 A step = one hipGraph replay of forward + decode + NMS over the batch, plus (N>1)
-one RCCL all-gather of the fixed-shape [B,300,6] box buffers.
+one RCCL all-gather of the per-image [det | count] records (ydbl.parallel).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model n|s|l] [--batch B] [--imgsz S] [--fp32]
 
@@ -160,10 +160,21 @@ def hg_fused_traffic(step, elsize):
     return 2 * n * dd * elsize, 2.0 * n * (dd * dd + 3 * e * dd) + 2.0 * d.x.n * e * dd * (2 * dd + 2 * dd)
 
 
+def lsk_traffic(step, elsize):
+    """ydbl_lsk_attn: a1, a2 read, attn = conv1(a1) | conv2(a2) written (+ per-pixel stats, left out);
+    ydbl_lsk_out: attn and x read, y = x * conv(gate(attn)) written (LSKA.py:43-52)."""
+    d = step.args[0]
+    p, dim = _px(d.x), d.x.c
+    if step.fn.__name__ == "ydbl_lsk_attn":
+        return 3 * p * dim * elsize, 2.0 * p * dim * dim
+    return 3 * p * dim * elsize, 2.0 * p * (dim // 2) * dim + 2.0 * p * 98 * 2
+
+
 TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("dsconv", dsconv_traffic),
            "ydbl_dysample2": ("dysample", dysample2_traffic), "ydbl_hg_fused": ("hypergraph", hg_fused_traffic),
            "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
-           "ydbl_dysample_ex": ("dysample", dysample_traffic)}
+           "ydbl_dysample_ex": ("dysample", dysample_traffic), "ydbl_lsk_attn": ("lsk", lsk_traffic),
+           "ydbl_lsk_out": ("lsk", lsk_traffic)}
 
 
 def roofline(session, dtype_name, key=None, step_ms=None):
@@ -392,16 +403,22 @@ def launch_ranks(n: int, argv: list[str]) -> int:
 
 def stub_step_factory(B: int, world: int, rank: int):
     """--stub-cpu: the multi-rank plumbing of a step (gloo, CPU) without a GPU -- each rank fills its
-    fixed-shape det/count buffers and takes part in the one all-gather.  Used by tests/test_bench_launch.py."""
-    from ydbl.parallel import gather_detections
+    record buffer (ydbl.parallel: [det | count] per image) and takes part in the one all-gather into a
+    preallocated global buffer.  Used by tests/test_bench_launch.py."""
+    from ydbl.parallel import GlobalDetections, gather_records, record_views, record_width
 
-    det = torch.full((B, 300, 6), float(rank))
-    cnt = torch.full((B,), rank + 1, dtype=torch.int32)
+    rec = torch.zeros(B, record_width(300))
+    det, cnt = record_views(rec, 300)
+    det.fill_(float(rank))
+    cnt.fill_(rank + 1)
+    out = torch.empty(world * B, rec.shape[1])
+    glob = GlobalDetections(out, B * world, world, 300)
 
     def step():
         if world > 1:
-            d, c = gather_detections(det, cnt, B * world)
-            assert d.shape[0] == B * world and int(c[-1]) == world
+            gather_records(rec, out)
+            d, c = glob.tensors()
+            assert d.shape[0] == B * world and int(c[-1]) == world and float(d[-1, 0, 0]) == world - 1
 
     return step
 
@@ -453,18 +470,20 @@ def main():
     load_trained(model.model, ROOT / "tests" / "golden" / fx)
     B, S = args.batch, args.imgsz
     fp8 = True if args.fp8 >= 1.0 else (args.fp8 if args.fp8 > 0 else False)
-    sess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=fp8,
-                         streams=args.streams)
+    from ydbl.parallel import ShardedPredictor
+
+    # this rank's B images of the global batch B * world; its NMS writes the per-image [det | count] records
+    # that the step's one all-gather ships (ydbl.parallel; no process group at N = 1: no collective)
+    sp = ShardedPredictor(model, B * world, S, S, dev, half=half, conf=0.25, iou=0.7, max_det=300, fp8=fp8,
+                          streams=args.streams)
+    sess = sp.session
     if args.fp8:  # activation scales from a separate synthetic calibration batch
         sess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
     # synthetic images, different per rank, resident in the session's input buffer (HBM)
-    sess.load(blob_images(B, S, seed=1234 + rank).to(dev))
-    from ydbl.parallel import gather_detections
+    sp.load(images_local=blob_images(B, S, seed=1234 + rank).to(dev))
 
     def step():
-        det, cnt = sess()  # this rank's B images: forward + decode + NMS (one hipGraph replay)
-        if world > 1:  # the path's only exchange: one all-gather of the fixed-shape box buffers
-            gather_detections(det, cnt, B * world)
+        sp.run()  # forward + decode + NMS (one hipGraph replay per sub-batch stream) [+ the one all-gather]
 
     el = timed_steps(step, args, world, lambda: torch.cuda.synchronize(dev), dev)
     key = workload_key(args, dtype_name)

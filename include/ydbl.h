@@ -42,7 +42,7 @@
  *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
  *   ydbl_lsk_attn/_out     <- LSKblock.forward LSKA.py:43-52 (conv1 | conv2 + stats; gate + conv + x *)
  *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708 (ydbl_hg_fused: the whole
- *                             AdaHGConv incl. pre_head_proj block.py:1645, one launch)
+ *                             AdaHGConv incl. pre_head_proj block.py:1645, one call)
  *   ydbl_detect_decode     <- Detect._inference head.py:143-181 + DFL block.py:79-83 +
  *                             make_anchors/dist2bbox utils/tal.py:333-357 + NMS candidate
  *                             filter utils/ops.py:234-276
@@ -257,10 +257,10 @@ int64_t ydbl_hg_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges)
 int ydbl_hg_context(const ydbl_hg_desc* d, void* stream);
 /* stage 2: logits, softmax over tokens, vertex->edge->vertex, residual (needs xp) */
 int ydbl_hg_propagate(const ydbl_hg_desc* d, void* stream);
-/* The whole AdaHGConv (block.py:1582-1708, pre_head_proj included: xp unused, pre_w/pre_b set) as three kernels
- * over (64-token slice, image) workgroups, the per-image reductions merged in-launch by each image's last slice;
- * head_dim 16, (dim, edges) in {64, 128} x {4, 8}.  workspace: ydbl_hg_fused_workspace() bytes, ZEROED once by
- * the caller (its arrival counters are left zeroed again after every call); -1 = unsupported shape. */
+/* The whole AdaHGConv (block.py:1582-1708, pre_head_proj included: xp unused, pre_w/pre_b set) as five plain
+ * kernels: three over (64-token slice, image) workgroups writing per-slice partials, two merging them (stream
+ * order is the only synchronisation); head_dim 16, (dim, edges) in {64, 128} x {4, 8}.  workspace:
+ * ydbl_hg_fused_workspace() bytes, uninitialised memory is fine; -1 = unsupported shape. */
 int64_t ydbl_hg_fused_workspace(int32_t n, int32_t tokens, int32_t dim, int32_t edges, int32_t dtype);
 int ydbl_hg_fused(const ydbl_hg_desc* d, void* stream);
 
@@ -302,7 +302,10 @@ typedef struct {
 int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream);
 
 /* Batched class-offset NMS over the candidates of ydbl_detect_decode.
- * out: fp32 [n][max_det][6] = x1,y1,x2,y2,conf,cls (kept, score order), out_count int32 [n].
+ * out: fp32 [n][max_det][6] = x1,y1,x2,y2,conf,cls (kept, score order; rows past the count zeroed),
+ * out_count int32 [n].  out_stride / count_stride (0 = dense): floats between images of out (>= max_det * 6)
+ * and int32s between images of out_count -- e.g. one record per image [max_det*6 floats | count | pad], so
+ * the boxes and counts of a batch-sharded predict travel in ONE all-gather (ydbl.parallel).
  * Semantics of U/utils/ops.py:278-310 + torchvision nms: candidates above max_nms are cut to the
  * max_nms highest scores; boxes offset by cls*max_wh (0 if agnostic); stable descending sort;
  * suppress j if IoU(i,j) > iou_thres (double compare); keep <= max_det.
@@ -317,6 +320,7 @@ typedef struct {
   float clip_w, clip_h;
   float* out; int32_t* out_count;
   void* workspace;
+  int64_t out_stride, count_stride;
 } ydbl_nms_desc;
 int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms);
 int ydbl_nms(const ydbl_nms_desc* d, void* stream);

@@ -1,6 +1,6 @@
 """Micro-benchmark of ydbl_conv2d_nhwc on the DBL-n 3x3 / 1x1 shapes (HIP-event timed, fp16, bs 32).
 
-    YDBL_NO_HALO=1 python scripts/conv_bench.py   # implicit-GEMM kernels only, for A/B
+
 """
 import os
 import sys

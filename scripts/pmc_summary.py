@@ -31,7 +31,8 @@ FAMILIES = {  # family -> (kernel-name keys, FETCH_SIZE multiplier)
     "stem": (("stem_kernel",), 2),
     "depthwise": (("dwconv_lds_kernel", "dwconv_kernel", "dw_pair_kernel"), 2),
     "hypergraph": (("hg_", "hg3_"), 2),
-    "dysample": (("dysample_kernel",), 2),
+    "dysample": (("dysample_kernel", "dysample2_kernel"), 2),
+    "lsk": (("lsk_attn_kernel", "lsk_out_kernel"), 2),
     "decode": (("decode_kernel",), 1),
     "nms": (("nms_kernel",), 1),
 }

@@ -70,12 +70,28 @@ def fp16_rule(st):
 
 
 def load_e2e(golden_dir, name):
+    """(y64 [R, 4+nc, A] fp64, meta); meta["y32"] = the oracle's own fp32 answer (y64 + the stored fp16 d32) when
+    the fixture carries it."""
     import json
 
     import numpy as np
 
     with np.load(golden_dir / f"e2e_{name}.npz", allow_pickle=False) as z:
-        return torch.from_numpy(z["y64"]).double(), json.loads(str(z["meta"]))
+        y64 = torch.from_numpy(z["y64"]).double()
+        meta = json.loads(str(z["meta"]))
+        if "d32" in z.files:
+            meta["y32"] = y64 + torch.from_numpy(z["d32"]).double()
+        return y64, meta
+
+
+def direct_report(yg, meta):
+    """|gpu - oracle fp32| (max box px, max score) on the reference images: the north_star's direct comparison,
+    reported beside the fp64 rule (the oracle's fp32 leg is itself ~1e-2 px from fp64 at these sizes)."""
+    y32 = meta.get("y32")
+    if y32 is None:
+        return None
+    d = (yg.double() - y32).abs()
+    return {"box_max": d[:, :4].max().item(), "conf_max": d[:, 4:].max().item()}
 
 
 @torch.inference_mode()

@@ -24,8 +24,9 @@ def test_cv1_fusable_dbl_n_shape(monkeypatch):
     assert m._cv3_fusable(plan, _x(16, 64))
     assert not m._cv1_fusable(NS(dtype=torch.float32), _x(16, 64))  # fp16 only
     assert not m._cv1_fusable(plan, _x(16, 64, cs=68))  # 16-byte pixel vectors
-    monkeypatch.setenv("YDBL_DS_LEAN", "0")  # the chunked kernel has no leading GEMM
+    monkeypatch.setenv("YDBL_DS_LEAN", "0")  # the chunked kernel has neither the leading nor the trailing GEMM
     assert not m._cv1_fusable(plan, _x(16, 64))
+    assert not m._cv3_fusable(plan, _x(16, 64))
     monkeypatch.delenv("YDBL_DS_LEAN")
     monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")
     assert not m._cv1_fusable(plan, _x(16, 64))
@@ -41,7 +42,9 @@ def test_cv1_fusable_only_at_64_channels_and_k3(monkeypatch):
     assert not M.C3(64, 64, 1)._cv1_fusable(plan, _x(16, 64))
 
 
-def test_cv3_fusable_small_map_rule_for_128_channels():
+def test_cv3_fusable_small_map_rule_for_128_channels(monkeypatch):
+    monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
+    monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
     plan = NS(dtype=torch.float16)
     m = M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)
     assert m._cv3_fusable(plan, _x(16, 128, 20, 20))      # 16 * 3 * 3 = 144 8x8 tiles <= 160

@@ -307,3 +307,78 @@ def test_nms_paths_agree_on_model_candidates(golden_dir, monkeypatch, groups):
         outs.append((out, cnt))
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], sess.count) and torch.equal(outs[0][0], sess.det)
+
+
+@pytest.mark.parametrize("half", [False, True])
+def test_detection_model_forward(golden_dir, half):
+    """§8(b): the reference caller AutoBackend.forward -> ``self.model(im)`` (U/nn/autobackend.py:503-528) gets
+    DetectionModel.forward's inference return ``(y, feats)`` (U/nn/tasks.py:109-172, head.py:108-118) from
+    ``YOLO(cfg).model(x)``: y [B, 4+nc, A] and the per-level maps [B, 64+nc, H, W], checked against the oracle's
+    (y, feats) under the fp32 / fp16 rule (parity_util); fresh tensors per call; CPU input refused."""
+    import copy
+
+    from parity_util import err_stats, fp16_rule, fp32_rule, oracle_legs
+    from ydbl.utils.synthetic import blob_images
+
+    p, o = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    x = blob_images(2, 160, seed=5)
+    legs = ("fp64", "fp16") if half else ("fp64", "fp32")
+    ys, _ = oracle_legs(o, x, legs)
+    y64 = ys["fp64"]
+    with torch.no_grad():
+        _, f64 = copy.deepcopy(o).double()(x.double())
+        _, fleg = (copy.deepcopy(o).half()(x.half()) if half else o(x))
+    xin = x.cuda().half() if half else x.cuda()
+    y, feats = p.model(xin)
+    assert y.dtype == xin.dtype and y.device == xin.device and tuple(y.shape) == tuple(y64.shape)
+    assert len(feats) == 3
+    leg = ys[legs[1]]
+    st, st_ref = err_stats(y.float().cpu(), y64), err_stats(leg, y64)
+    tb, tc = (fp16_rule if half else fp32_rule)(st_ref)
+    print(f"forward {'fp16' if half else 'fp32'}: |y - fp64| box {st['box_max']:.3g} px (oracle leg "
+          f"{st_ref['box_max']:.3g}), score {st['conf_max']:.3g} ({st_ref['conf_max']:.3g}); |y - oracle leg| box "
+          f"{(y.float().cpu() - leg).abs()[:, :4].max().item():.3g} px")
+    key = "box_p999" if half else "box_max"
+    assert st[key] <= tb and st["conf_p999" if half else "conf_max"] <= tc, (st, st_ref)
+    for f, a64, al in zip(feats, f64, fleg):
+        assert f.shape == a64.shape and f.dtype == xin.dtype and f.is_contiguous()
+        dev_ref = (al.double() - a64).abs().max().item()
+        dev = (f.double().cpu() - a64).abs().max().item()
+        assert dev <= 2 * dev_ref + (2e-2 if half else 1e-3), (dev, dev_ref)
+    y2, feats2 = p.model(xin)
+    assert y2.data_ptr() != y.data_ptr() and torch.equal(y2, y) and all(torch.equal(a, b) for a, b in zip(feats, feats2))
+    with pytest.raises(RuntimeError):
+        p.model(x)
+
+
+def test_sharded_predictor_nccl_world1(golden_dir, tmp_path):
+    """The batch-sharded path with its one collective on RCCL: a world-size-1 "nccl" process group (FileStore), a
+    ShardedPredictor over DBL-n bs4 at 640 whose NMS writes the [det | count] records and whose all_gather_into_tensor
+    runs on RCCL; the gathered global detections are bit-equal to the plain session's (U/engine/trainer.py:222-227
+    is the reference's process-group setup)."""
+    import torch.distributed as dist
+
+    from ydbl.parallel import ShardedPredictor
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    x = blob_images(4, 640, seed=11).cuda()
+    refs = {}
+    for streams in (1, 2):  # the plain session of the same layout (one bs4 graph / two bs2 graphs)
+        plain = p.session(4, 640, 640, half=True, conf=0.25, iou=0.7, streams=streams)
+        refs[streams] = tuple(t.clone() for t in plain(x))
+    store = dist.FileStore(str(tmp_path / "store"), 1)
+    dist.init_process_group("nccl", rank=0, world_size=1, store=store)
+    try:
+        for streams in (1, 2):
+            sp = ShardedPredictor(p, 4, 640, 640, torch.device("cuda", 0), half=True, conf=0.25, iou=0.7,
+                                  streams=streams)
+            det, cnt = sp(images_global=x)
+            torch.cuda.synchronize()
+            det_ref, cnt_ref = refs[streams]
+            assert sp.distributed and det.shape == (4, 300, 6) and cnt.dtype == torch.int32
+            assert torch.equal(cnt.cpu(), cnt_ref.cpu()) and int(cnt.sum()) > 0
+            assert torch.equal(det.cpu(), det_ref.cpu())
+            assert det.data_ptr() == sp.gathered.data_ptr()  # views of the gathered buffer, no copy
+    finally:
+        dist.destroy_process_group()

@@ -532,12 +532,8 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // 12.6 -> 11.3 us at 1024; K 64 keeps 2048 there, 64->128 @80^2 14.4 vs 15.6 us -- and 64x64 tiles for the
   // deep-K (>= 512) 3x3 convs with >= 16384 output pixels: 64->64 s2 @80^2 14.6 -> 13.1 us; DBL-n bs32 on two
   // streams 16.20 -> 16.30 k img/s over three pairs with the halo kernel's n2_below 512, DBL-s bs64 even)
-  static const char* ov = getenv("YDBL_IGEMM_WANT");  // A/B knob for the benches
-  static const bool r2 = getenv("YDBL_IGEMM_R2") == nullptr;  // A/B knob (read once per process): round-2 rule
-  const int64_t big = r2 ? 131072 : 65536;
-  const int64_t want = ov && *ov ? atoi(ov)
-                                 : (a.Cout <= 128 && a.P <= 65536 ? 512
-                                    : (a.K <= 128 && a.P > (a.K <= 64 ? 65536 : big) ? 2048 : 1024));
+  const int64_t want = a.Cout <= 128 && a.P <= 65536 ? 512
+                       : (a.K <= 128 && a.P > (a.K <= 64 ? 65536 : 131072) ? 2048 : 1024);
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   if (a.Cout <= 16) {
     if (blocks(256, 16) >= want) return launch_igemm<T, Q8, 256, 16, 4, 1>(a, pointwise, s);
@@ -551,7 +547,7 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   }
   if (a.Cout <= 64) {
     if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
-    if (blocks(64, 64) >= want || (r2 && !pointwise && a.K >= 512 && a.P >= 16384))
+    if (blocks(64, 64) >= want || (!pointwise && a.K >= 512 && a.P >= 16384))
       return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
     return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
   }
@@ -559,26 +555,19 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   // once per column block, from L2/MALL at these map sizes).  Measured against 128-wide blocks on the
   // bench workloads: DBL-n bs32 14.82 -> 14.91 k img/s (bs16 graphs: 64->128 @80^2 22.6 -> 19.8 us,
   // 128->192 @40^2 15.6 -> 12.1 us), DBL-s bs64 7.52 -> 7.57 k, DBL-l 1280 bs8 467 -> 466 (noise).
-  static const char* b64 = getenv("YDBL_IGEMM_BN64");  // A/B knob (read once per process): 0 = 128-wide column blocks
-  if (!(b64 && *b64 == '0')) {
-    if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
-    if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
-    return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
-  }
-  if (blocks(128, 128) >= want) return launch_igemm<T, Q8, 128, 128, 2, 2>(a, pointwise, s);
-  if (blocks(64, 128) >= want) return launch_igemm<T, Q8, 64, 128, 2, 2>(a, pointwise, s);
-  return launch_igemm<T, Q8, 32, 128, 2, 2>(a, pointwise, s);
+  if (blocks(128, 64) >= want) return launch_igemm<T, Q8, 128, 64, 2, 2>(a, pointwise, s);
+  if (blocks(64, 64) >= want) return launch_igemm<T, Q8, 64, 64, 2, 2>(a, pointwise, s);
+  return launch_igemm<T, Q8, 32, 64, 2, 2>(a, pointwise, s);
 }
 
 // Kernel choice: thin-input spatial tile (f16/f32 only), halo tile, wave-split-K, block GEMM.
 template <typename T, bool Q8>
 static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
-  static const bool no_halo = getenv("YDBL_NO_HALO") != nullptr;  // A/B switch for scripts/conv_bench.py
   if constexpr (sizeof(T) == 2 && !Q8) {
-    if (!no_halo && try_conv3x3_vw(a, kh, s)) return;
+    if (try_conv3x3_vw(a, kh, s)) return;
   }
   if (!Q8 && try_tile<T>(a, kh, s)) return;
-  if (!no_halo && try_conv3x3_halo<T, Q8>(a, kh, s)) return;
+  if (try_conv3x3_halo<T, Q8>(a, kh, s)) return;
   if (try_wsk<T, Q8>(a, pw, s)) return;
   dispatch_conv<T, Q8>(a, pw, s);
 }

@@ -161,9 +161,8 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
   // most CUs with one workgroup; 32-channel slices double the grid (conv_bench.py bs16: 384->64 @40^2
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
-  static const char* ev = getenv("YDBL_HALO_N2");  // A/B knob (read once per process)
   // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench)
-  const int64_t n2_below = ev && *ev ? atoll(ev) : 512;
+  constexpr int64_t n2_below = 512;
   if (a.Cout <= 32) {
     conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
@@ -185,30 +184,23 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
 template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   constexpr int BK = 4 * Vec<T>::N;
-  // Stride 2 on >= 204800 output pixels: 8-row tiles over a (2*8+1) x 33 halo (YDBL_NO_HALO_S2 A/B:
-  // DBL-l 128->256 @320 bs8 442 -> 341 us).  Smaller maps stay on the block GEMM: 128->128 @40 bs32
+  // Stride 2 on >= 204800 output pixels: 8-row tiles over a (2*8+1) x 33 halo (A/B against the block
+  // GEMM: DBL-l 128->256 @320 bs8 442 -> 341 us).  Smaller maps stay on the block GEMM: 128->128 @40 bs32
   // 17.8 vs 24.7 us, and DBL-n's 64->64 @80 bs32 (18.8 vs 17.5 us alone) cost the whole step ~40 us.
-  static const bool no_s2 = getenv("YDBL_NO_HALO_S2") != nullptr;
-  if (!no_s2 && kh == 3 && a.KW == 3 && a.PAD == 1 && a.DIL == 1 && a.S == 2 && a.Cin % BK == 0 &&
+  if (kh == 3 && a.KW == 3 && a.PAD == 1 && a.DIL == 1 && a.S == 2 && a.Cin % BK == 0 &&
       a.Cin >= 2 * BK && a.xcs % Vec<T>::N == 0 && (int64_t)a.P >= 204800)
     return launch_halo<T, Q8, 2, 8>(a, s), true;
   if (kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
   if (a.Cin % BK || a.Cin < 2 * BK || a.xcs % Vec<T>::N) return false;
-  static const char* fth = getenv("YDBL_HALO_TH");  // A/B knob for scripts/conv_bench.py: force 4/8/16-row tiles
-  const int force_th = fth && *fth ? atoi(fth) : 0;
-  static const char* mp = getenv("YDBL_HALO_MINP");  // A/B knob (read once per process): smallest output-pixel count routed here
   // 51200 output pixels (40^2 x 32) was the measured crossover at bs32; the bench's two bs16 sub-batch
   // graphs put the 40^2 head convs at 25600, where the halo tile still wins (DBL-n bs32 on two streams
   // 13.7 k -> 14.1 k img/s; 12800 loses again: 14.0 k)
-  if ((int64_t)a.P < (mp && *mp ? atoll(mp) : 25600)) return false;
-  if (force_th == 4) return launch_halo<T, Q8, 1, 4>(a, s), true;
-  if (force_th == 8) return launch_halo<T, Q8, 1, 8>(a, s), true;
-  if (force_th == 16) return launch_halo<T, Q8, 1, 16>(a, s), true;
+  if ((int64_t)a.P < 25600) return false;
   const int64_t csplit = cdiv(a.Cout, 64);
   const int64_t tiles8 = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * csplit;
   const int64_t tiles16 = (int64_t)a.N * cdiv(a.Ho, 16) * cdiv(a.Wo, 16) * csplit;
   // No 4-row tiles by default: every workgroup re-reads all of its channels' weights, so at 480
-  // 8-row tiles (40^2 bs32, Cout 64) the doubled grid lost (YDBL_HALO_TH A/B: 384->64 88.9 vs
+  // 8-row tiles (40^2 bs32, Cout 64) the doubled grid lost (A/B: 384->64 88.9 vs
   // 49.6 us, 192->64 45.9 vs 28.0 us); 384->64 @40^2 also beats the wave-split-K kernel it used to
   // take (78.8 us).  (P >= 51200 already guarantees >= 400 8-row tiles.)
   (void)tiles8;
@@ -342,12 +334,10 @@ static void launch_vw(const ConvArgs<_Float16>& a, int cs, hipStream_t s) {
 // re-read loses (measured with the kernel open to Cin/Cout 32..128: 64->64 @80^2 41.7 -> 47.9,
 // 64->32 @80^2 22.5 -> 39.5, 64->128 @40^2 26.0 -> 29.4, 64->64 @20^2 8.9 -> 10.0 us).
 bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
-  static const bool off = getenv("YDBL_NO_VW") != nullptr;  // A/B switch for scripts/conv_bench.py
-  if (off || kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
+  if (kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
   if (a.xcs % 8 || a.H != a.Ho || a.W != a.Wo || (int64_t)a.N * a.Ho * a.Wo >= (1LL << 31)) return false;
   if (a.Cin == 128 && a.Cout == 64) return launch_vw<128, 1, 4, 2>(a, 1, s), true;
-  static const char* vm = getenv("YDBL_VW_MINP");  // A/B knob (read once per process)
-  const int64_t vw_min = vm && *vm ? atoll(vm) : 25601;
+  constexpr int64_t vw_min = 25601;
   if (a.Cin == 64 && a.Cout == 64 && a.P >= vw_min && a.P <= 65536) return launch_vw<64, 2, 2, 4>(a, 1, s), true;
   return false;
 }

@@ -206,6 +206,7 @@ struct NmsArgs {
   double thr; int max_det, max_nms; float off_scale;
   float clip_w, clip_h;
   float* out; int* out_count;
+  int64_t ostride; int64_t cstride;  // floats per image of out, int32s per image of out_count
 };
 
 // bitonic sort of P (power of two) key/value pairs; keys/vals in LDS or global, one workgroup
@@ -844,15 +845,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       v[1] = fminf(fmaxf(v[1], 0.f), p.clip_h);
       v[3] = fminf(fmaxf(v[3], 0.f), p.clip_h);
     }
-    float* dst = p.out + ((int64_t)b * p.max_det + k) * 6;
+    float* dst = p.out + (int64_t)b * p.ostride + (int64_t)k * 6;
     dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
     dst[4] = p.cscore[o];
     dst[5] = float(p.ccls[o]);
   }
   // rows kept..max_det of the fixed-shape output are zeroed (the all-gather ships whole buffers)
-  float* rest = p.out + ((int64_t)b * p.max_det + kept) * 6;
+  float* rest = p.out + (int64_t)b * p.ostride + (int64_t)kept * 6;
   for (int k = threadIdx.x; k < (p.max_det - kept) * 6; k += NMS_THREADS) rest[k] = 0.f;
-  if (threadIdx.x == 0) p.out_count[b] = kept;
+  if (threadIdx.x == 0) p.out_count[(int64_t)b * p.cstride] = kept;
 }
 
 // The groups' keep lists of one image, each in (score, index) order, merged into the first max_det rows:
@@ -914,15 +915,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_merge_kernel(NmsArgs p) {
       v[1] = fminf(fmaxf(v[1], 0.f), p.clip_h);
       v[3] = fminf(fmaxf(v[3], 0.f), p.clip_h);
     }
-    float* dst = p.out + ((int64_t)b * p.max_det + rank) * 6;
+    float* dst = p.out + (int64_t)b * p.ostride + (int64_t)rank * 6;
     dst[0] = v[0]; dst[1] = v[1]; dst[2] = v[2]; dst[3] = v[3];
     dst[4] = p.cscore[o];
     dst[5] = float(p.ccls[o]);
   }
   const int kept = min(E, p.max_det);
-  float* rest = p.out + ((int64_t)b * p.max_det + kept) * 6;
+  float* rest = p.out + (int64_t)b * p.ostride + (int64_t)kept * 6;
   for (int k = threadIdx.x; k < (p.max_det - kept) * 6; k += NMS_THREADS) rest[k] = 0.f;
-  if (threadIdx.x == 0) p.out_count[b] = kept;
+  if (threadIdx.x == 0) p.out_count[(int64_t)b * p.cstride] = kept;
 }
 
 // Zeroes the per-image candidate counters ahead of the decode's atomics.  A kernel, not
@@ -1030,6 +1031,8 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   if (d->max_det < 1 || d->max_det > NMS_MAX_DET) return fail(YDBL_EINVAL, "nms: max_det must be in [1, 4096]");
   if (d->max_nms < 1 || d->max_nms > NMS_MAX_FLAGS) return fail(YDBL_EINVAL, "nms: max_nms must be in [1, 32768]");
   if (!(d->iou_thres >= 0.0 && d->iou_thres <= 1.0)) return fail(YDBL_EINVAL, "nms: iou_thres must be in [0, 1]");
+  if (d->out_stride < 0 || (d->out_stride && d->out_stride < (int64_t)d->max_det * 6) || d->count_stride < 0)
+    return fail(YDBL_EINVAL, "nms: out_stride must be 0 or >= max_det * 6, count_stride >= 0");
   hipStream_t s = as_stream(stream);
   NmsArgs a;
   a.cbox = d->cand_box; a.cscore = d->cand_score; a.ccls = d->cand_cls; a.cidx = d->cand_idx;
@@ -1046,6 +1049,8 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   a.off_scale = d->agnostic ? 0.f : d->max_wh;
   a.clip_w = d->clip_w; a.clip_h = d->clip_h;
   a.out = d->out; a.out_count = d->out_count;
+  a.ostride = d->out_stride ? d->out_stride : (int64_t)d->max_det * 6;
+  a.cstride = d->count_stride ? d->count_stride : 1;
   a.frows = nms_fast_rows(d->cap);
   a.fmask = reinterpret_cast<uint64_t*>(a.gcount + (int64_t)d->n * NMS_GROUPS + ((int64_t)d->n * NMS_GROUPS & 1));
   a.frank = reinterpret_cast<int*>(a.fmask + (int64_t)d->n * a.frows * NMS_FW);

@@ -218,10 +218,6 @@ static void launch_ds_tile(const ConvArgs<T>& a, const float* dww, const float* 
     const int cs = (int)cdiv(a.Cout, ntn * 16);
     kern<<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, dww, dwb, dw_act, tiles_x, tiles_y, cs);
   };
-  static const char* fn = getenv("YDBL_DS_NTN");  // A/B knob for scripts/ds_bench.py: force 2/4 output tiles
-  const int force = fn && *fn && !a.t3w ? atoi(fn) : 0;  // the tail needs every channel in one wave
-  if (force == 2) return go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
-  if (force == 4) return go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 4, DBUF>, 4);
   if (a.Cout <= 32) go(dsconv_kernel<T, K, S, DIL, TH, TW, CSEG, 2, DBUF>, 2);
   // k3 s1 with < 512 tiles: two 64-channel column workgroups per tile (the cheap depthwise phase is
   // recomputed; 128->128 @20^2 bs32 15.0 -> 11.8 us; k7 loses: 19.7 -> 25.4)
@@ -239,16 +235,12 @@ static int launch_ds(const ConvArgs<T>& a, const float* dww, const float* dwb, i
   if constexpr (sizeof(T) == 2) {
     if (try_dsc_lean(a, dww, dwb, dw_act, K, S, DIL, s)) return check_launch("ydbl_dsconv_nhwc");
   }
-  static const char* tv = getenv("YDBL_DS_TILE");  // A/B knob for scripts/ds_bench.py: 8 = 8x8 everywhere, S = 8x8 single-buffered
-  const char t = tv && *tv ? tv[0] : 'A';
   // Fewer than 400 16x8 tiles (the bench's bs16 sub-batch graphs at 40^2: 240): 8x8 single-buffered
   // tiles, 1.7x the workgroups (DBL-n bs32 on two streams 13.98 k -> 14.45 k img/s; at bs32 / 480 tiles
   // the two are even, and the 16x8 tile stays ahead on DBL-s bs64 and DBL-l 1280)
   const int64_t t168 = (int64_t)a.N * cdiv(a.Ho, 16) * cdiv(a.Wo, 8);
-  static const char* tl = getenv("YDBL_DS_T168");  // A/B knob (read once per process)
-  const int64_t t168_max = tl && *tl ? atoll(tl) : 400;
-  if (t == 'S' || (t == 'A' && a.Wo > 20 && t168 < t168_max)) launch_ds_tile<T, K, S, DIL, 8, 8, 2, false>(a, dww, dwb, dw_act, s);
-  else if (a.Wo > 20 && t != '8') launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, dwb, dw_act, s);
+  if (a.Wo > 20 && t168 < 400) launch_ds_tile<T, K, S, DIL, 8, 8, 2, false>(a, dww, dwb, dw_act, s);
+  else if (a.Wo > 20) launch_ds_tile<T, K, S, DIL, 16, 8, 4, false>(a, dww, dwb, dw_act, s);
   else launch_ds_tile<T, K, S, DIL, 8, 8, 2, true>(a, dww, dwb, dw_act, s);
   return check_launch("ydbl_dsconv_nhwc");
 }

@@ -194,15 +194,11 @@ extern "C" int ydbl_dysample2(const ydbl_dysample2_desc* d, void* stream) {
   hipStream_t s = as_stream(stream);
   // 2 x 8 tiles (kbench bs16, in graph: 128@40 20.4 us as offset conv + dysample_ex -> 18.2 with 8 x 8 tiles,
   // 16.4 with 4 x 8, 15.4 with 2 x 8; 256@20 15.6 -> 13.8 / 13.8 / 11.3): the halo re-read costs less than
-  // the parallelism small tiles buy.  YDBL_DS2_TH: A/B knob (read per launch), tile rows 8 / 4 / 2.
-  static const char* ev = getenv("YDBL_DS2_TH");  // A/B knob (read once per process)
-  const int th = ev && *ev ? atoi(ev) : 2;
+  // the parallelism small tiles buy.
   if (d->x.dtype == YDBL_F16) {
-    if (C == 64) return th == 4 ? ds2_go<_Float16, 64, 4, 8>(d, s) : th == 8 ? ds2_go<_Float16, 64, 8, 8>(d, s)
-                                                                   : ds2_go<_Float16, 64, 2, 8>(d, s);
-    if (C == 128) return th == 4 ? ds2_go<_Float16, 128, 4, 8>(d, s) : th == 8 ? ds2_go<_Float16, 128, 8, 8>(d, s)
-                                                                     : ds2_go<_Float16, 128, 2, 8>(d, s);
-    if (C == 256) return th == 4 ? ds2_go<_Float16, 256, 4, 8>(d, s) : ds2_go<_Float16, 256, 2, 8>(d, s);
+    if (C == 64) return ds2_go<_Float16, 64, 2, 8>(d, s);
+    if (C == 128) return ds2_go<_Float16, 128, 2, 8>(d, s);
+    if (C == 256) return ds2_go<_Float16, 256, 2, 8>(d, s);
   } else {
     if (C == 64) return ds2_go<float, 64, 8, 8>(d, s);
     if (C == 128) return ds2_go<float, 128, 4, 8>(d, s);

@@ -1,17 +1,19 @@
-// AdaHGConv (U/nn/modules/block.py:1582-1708: AdaHyperedgeGen + AdaHGConv, pre_head_proj included) in four
-// launches spread over the chip (every DBL call: N = 1600 tokens at 640, D = 64 / 128, E = 4 / 8, head_dim 16).
-// The math has three reductions over all N tokens of an image (context stats, softmax over N, He = A^T X);
-// each launch splits the tokens into slices of HG3_TS, one 256-thread workgroup per (slice, image), and the
-// workgroup that finishes an image's reduction last (sc1 slab hand-off, conv_common.hpp) runs the small
-// per-image tail:
-//   hg3_ctx   partial [sum | max] of X per slice -> last: ctx;
-//   hg3_proto proto = base + Wc ctx + bc (16 rows per workgroup: the 2D x E*D weight is read by many CUs at once);
+// AdaHGConv (U/nn/modules/block.py:1582-1708: AdaHyperedgeGen + AdaHGConv, pre_head_proj included) in five
+// plain launches spread over the chip (every DBL call: N = 1600 tokens at 640, D = 64 / 128, E = 4 / 8,
+// head_dim 16).  The math has three reductions over all N tokens of an image (context stats, softmax over N,
+// He = A^T X); the token-parallel launches split the tokens into slices of HG3_TS, one 256-thread workgroup
+// per (slice, image), write per-slice partials to the workspace, and the next launch merges them (stream
+// order is the only synchronisation: no counters, nothing to zero):
+//   hg3_ctx   partial [sum | max] of X per slice;
+//   hg3_proto merges the slices' [sum | max] into ctx, then proto = base + Wc ctx + bc (16 rows per workgroup:
+//             the 2D x E*D weight is read by many CUs at once);
 //   hg3_edge  xp = X Wp^T + bp (MFMA, rounded as the unfused conv stores it), logits = mean_h(xp_h . proto_h) / 4
 //             (kept in the workspace), per-slice online-softmax partials (max m_s, sum of exp, He'_s =
-//             sum exp(l - m_s) X) -> last: m, 1/S, He = sum_s e^(m_s - m) He'_s / S, He2 = GELU(He We^T + be),
+//             sum exp(l - m_s) X);
+//   hg3_merge per (image, hyperedge): m, 1/S, He = sum_s e^(m_s - m) He'_s / S, He2 = GELU(He We^T + be),
 //             He3 = He2 Wn^T (node_proj re-associated);
 //   hg3_out   y = GELU(A He3 + bn) + X, A = exp(l - m) / S.
-// (One 1024-thread workgroup per image doing all of it -- the previous form -- kept 16 CUs busy for 58 us per
+// (One 1024-thread workgroup per image doing all of it -- the round-2 form -- kept 16 CUs busy for 58 us per
 // call at bs16 while the rest of the chip waited.)  All arithmetic fp32; slices merge in slice order.
 #include "conv_common.hpp"
 
@@ -33,14 +35,13 @@ struct Hg3 {
 
 // workspace carve-up (bytes, 256-aligned sections)
 struct Hg3Ws {
-  int64_t cnt, slab1, ctx, proto, logits, slab2, he3, stat, total;
+  int64_t slab1, ctx, proto, logits, slab2, he3, stat, total;
 };
 static Hg3Ws hg3_ws(int B, int N, int D, int E) {
   auto up = [](int64_t v) { return (v + 255) & ~255ll; };
   const int NS = (N + HG3_TS - 1) / HG3_TS, R2 = (2 * E + E * D + 3) / 4 * 4;
   Hg3Ws w;
-  w.cnt = 0;
-  w.slab1 = up(w.cnt + 2LL * B * 4);
+  w.slab1 = 0;
   w.ctx = up(w.slab1 + (int64_t)B * NS * 2 * D * 4);
   w.proto = up(w.ctx + (int64_t)B * 2 * D * 4);
   w.logits = up(w.proto + (int64_t)B * E * D * 4);

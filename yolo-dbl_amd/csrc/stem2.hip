@@ -337,13 +337,9 @@ extern "C" int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream) {
     return check_launch("ydbl_conv_stem2");
   };
   const bool v4 = d->w % 4 == 0 && (reinterpret_cast<uintptr_t>(d->x) & 15) == 0;
-  static const char* ev = getenv("YDBL_STEM2_TH");  // A/B knob (read once per process): 4 / 16-row tiles
-  const int th = ev && *ev ? atoi(ev) : 8;
 #define YDBL_STEM2_GO(C0_, TH_)                                                                                     \
   return v4 ? go(stem2_kernel<C0_, 32, TH_, true>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)                           \
             : go(stem2_kernel<C0_, 32, TH_, false>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)
-  if (c0 == 8 && th == 4) YDBL_STEM2_GO(8, 4);
-  if (c0 == 8 && th == 16) YDBL_STEM2_GO(8, 16);
   if (c0 == 8) YDBL_STEM2_GO(8, 8);
   if (c0 == 16) YDBL_STEM2_GO(16, 8);
 #undef YDBL_STEM2_GO

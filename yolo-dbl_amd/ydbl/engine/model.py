@@ -154,16 +154,17 @@ class Model:
 
     def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
                 multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True,
-                streams=1) -> DetectSession:
+                streams=1, gather_rows=None, nms=True) -> DetectSession:
         """A compiled (batch, h, w, dtype, NMS settings) inference session; streams > 1 splits the batch into
         that many concurrently replayed sub-batch graphs (DetectSession)."""
         dev = select_device(device)
         dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
-               float(fp8), bool(clip), int(streams),
-               # the kernels' A/B routing knobs are read at launch time, so a captured graph keeps the routing
-               # of its capture: a different knob setting is a different session
+               float(fp8), bool(clip), int(streams), gather_rows, bool(nms),
+               # the remaining YDBL_* switches (plan-builder fusions in ydbl.nn.modules; YDBL_DS_LEAN / YDBL_NMS_*
+               # in the C-ABI) are read at plan build or at each launch, so a captured graph keeps the routing of
+               # its capture: a different switch setting is a different session
                tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("YDBL_"))))
         s = self._sessions.get(key)
         if s is None:
@@ -172,7 +173,7 @@ class Model:
             with torch.cuda.device(dev):
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
                                   keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip,
-                                  streams=streams)
+                                  streams=streams, gather_rows=gather_rows, nms=nms)
             self._sessions[key] = s
         else:
             self._sessions.move_to_end(key)

@@ -27,7 +27,8 @@ class DetectSession:
 
     def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
                  multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
-                 keep_pred=False, use_graph=True, device="cuda", fp8=False, streams=1, _outputs=None):
+                 keep_pred=False, use_graph=True, device="cuda", fp8=False, streams=1, gather_rows=None, nms=True,
+                 _outputs=None):
         if fp8 and dtype != torch.float16:
             raise ValueError("fp8 operands run on the fp16 activation path (half=True)")
         self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
@@ -37,9 +38,24 @@ class DetectSession:
         self.fp8_fraction = float(fp8) if not isinstance(fp8, bool) and 0 < float(fp8) < 1 else 1.0
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         self.children = []
+        self.records = None
+        if _outputs is None and gather_rows is not None:
+            # one record per image [det (max_det*6 fp32) | count (int32) | pad]: the boxes and counts of a batch-
+            # sharded predict leave the GPU in ONE all-gather (ydbl.parallel); rows >= batch stay empty padding
+            from ..parallel import record_views, record_width
+
+            if gather_rows < batch:
+                raise ValueError(f"gather_rows {gather_rows} < batch {batch}")
+            self.records = torch.zeros((gather_rows, record_width(self.max_det)), dtype=torch.float32,
+                                       device=torch.device(device))
+            det_v, cnt_v = record_views(self.records[:batch], self.max_det)
+            nc_ = model.model[-1].nc
+            A_ = sum((h // int(st)) * (w // int(st)) for st in model.model[-1].stride.tolist())
+            _outputs = (det_v, cnt_v,
+                        torch.empty((batch, 4 + nc_, A_), dtype=torch.float32, device=device) if keep_pred else None)
         if streams > 1 and batch >= streams:
             self._init_split(model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes, max_nms,
-                             max_wh, clip, keep_pred, use_graph, device, fp8, streams)
+                             max_wh, clip, keep_pred, use_graph, device, fp8, streams, nms, _outputs)
             return
         cm = model.compile(batch, h, w, dtype, device=device)
         self.compiled = cm
@@ -79,30 +95,35 @@ class DetectSession:
         nd = NmsDesc(self.cand_box.data_ptr(), self.cand_score.data_ptr(), self.cand_cls.data_ptr(),
                      self.cand_idx.data_ptr(), self.cand_count.data_ptr(), batch, cap, self.iou, self.max_det,
                      int(max_nms), int(bool(agnostic)), float(max_wh), float(w) if clip else 0.0,
-                     float(h) if clip else 0.0, self.det.data_ptr(), self.count.data_ptr(), ws.data_ptr())
-        plan.launch("ydbl_nms", nd, what="NMS", keep=[nd])
+                     float(h) if clip else 0.0, self.det.data_ptr(), self.count.data_ptr(), ws.data_ptr(),
+                     self.det.stride(0), self.count.stride(0))
+        if nms:  # nms=False: forward + decode only (DetectionModel.forward -> (y, feats))
+            plan.launch("ydbl_nms", nd, what="NMS", keep=[nd])
         self.plan = plan
         self.plans = [plan]
         self.use_graph = use_graph
         self._graph = None
 
     def _init_split(self, model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes, max_nms,
-                    max_wh, clip, keep_pred, use_graph, device, fp8, streams):
+                    max_wh, clip, keep_pred, use_graph, device, fp8, streams, nms, outputs):
         from ..parallel import shard_bounds
 
         dev = torch.device(device)
         det = model.model[-1]
         nc = det.nc
         A = sum((h // int(s)) * (w // int(s)) for s in det.stride.tolist())
-        self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
-        self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
-        self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
+        if outputs is not None:
+            self.det, self.count, self.pred = outputs
+        else:
+            self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
+            self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+            self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
         self.bounds = [shard_bounds(batch, streams, r) for r in range(streams)]
         for a, b in self.bounds:
             outs = (self.det[a:b], self.count[a:b], self.pred[a:b] if keep_pred else None)
             self.children.append(DetectSession(model, b - a, h, w, dtype, conf, iou, max_det, multi_label, agnostic,
                                                classes, max_nms, max_wh, clip, keep_pred, use_graph, device, fp8,
-                                               _outputs=outs))
+                                               nms=nms, _outputs=outs))
         self.streams = [torch.cuda.Stream(dev) for _ in self.children]
         self.plans = [c.plan for c in self.children]
         self.plan = self.plans[0]

@@ -59,7 +59,10 @@ def frames_from_images(source):
             s = str(im)
             if s.lower().startswith(("http://", "https://")):
                 raise ValueError(f"URL sources need the network, which this framework does not use: {s}")
-            im = Image.open(s)  # autocast_list opens paths as PIL images (no EXIF transpose there)
+            with Image.open(s) as f:  # autocast_list opens paths as PIL images (no EXIF transpose there)
+                paths.append(s)
+                frames.append(pil_to_bgr(f))
+            continue
         if _is_pil(im):
             paths.append(getattr(im, "filename", "") or f"image{i}.jpg")
             frames.append(pil_to_bgr(im))

@@ -63,6 +63,13 @@ def _act_code(act) -> int:
     raise NotImplementedError(f"activation {type(act).__name__} has no HIP epilogue")
 
 
+def vec_aligned(v: TV) -> bool:
+    """The 16-byte channel-vector rule of check_view(need_vec_align) (csrc/capi.hip): channel count, channel
+    stride and base pointer all in whole 16-byte vectors."""
+    vec = 16 // v.base.element_size()
+    return v.c % vec == 0 and v.cs % vec == 0 and v.ptr % 16 == 0
+
+
 def _null_view() -> View:
     return View(None, 0, 0, 0, 0, 0, 0)
 
@@ -575,7 +582,10 @@ class C3(nn.Module):
         """cv3 can run as the trailing GEMM of the last bottleneck's k7 DSConv (dsc_lean.hip, ydbl_dsconv_desc.g2):
         fp16, m = DSBottlenecks ending in a k7 stride-1 DSConv with c_ in {64, 128} in and out, cv3 a 1x1 SiLU
         Conv 2c_ -> c_ (DSC3k with e = 1, U/nn/modules/block.py:1447-1503)."""
-        if plan.dtype != torch.float16 or os.environ.get("YDBL_NO_CV3_FUSE") or not len(self.m):
+        # the trailing GEMM runs only in the lean kernel (dsc_lean.hip): with it switched off the chunked kernel
+        # would refuse the g2 descriptor, so the rule must agree with _cv1_fusable's
+        if (plan.dtype != torch.float16 or os.environ.get("YDBL_NO_CV3_FUSE") or os.environ.get("YDBL_DS_LEAN") == "0"
+                or not len(self.m)):
             return False
         last, c_ = self.m[-1], self.cv1.conv.out_channels
         if not isinstance(last, DSBottleneck):
@@ -730,7 +740,7 @@ class AdaHGConv(nn.Module):
             # over (token slice, image) workgroups)
             pw = c(g.pre_head_proj.weight.detach().float().to(plan.dtype).contiguous())
             pb = c(g.pre_head_proj.bias.detach().float())
-            ws = plan.scratch(nws, zero=True)  # arrival counters start at zero; the kernels leave them there
+            ws = plan.scratch(nws)  # per-slice partials, fully written before they are read
             d = HgDesc(x.struct(), _null_view(), y.struct(), E, g.num_heads, *[t.data_ptr() for t in p], ws.data_ptr(),
                        pw.data_ptr(), pb.data_ptr())
             plan.launch("ydbl_hg_fused", d, what="AdaHG.fused", keep=[d, pw, pb, ws, *p])
@@ -900,9 +910,11 @@ class DySample(nn.Module):
         # offset = 0.25 * conv1x1(x) + init_pos  ->  folded into the conv weights/bias (0.25 is exact)
         w = self.offset.weight.detach().float().cpu() * 0.25
         b = self.offset.bias.detach().float().cpu() * 0.25 + self.init_pos.detach().float().cpu().view(-1)
-        if not os.environ.get("YDBL_DS2_OFF") and self.groups == 4 and x.c in (64, 128, 256):
-            # offset conv + sample in one launch (csrc/dysample2.hip), bit-identical to the pair below
-            y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)
+        y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)
+        if (not os.environ.get("YDBL_DS2_OFF") and self.groups == 4 and x.c in (64, 128, 256)
+                and vec_aligned(x) and vec_aligned(y)):
+            # offset conv + sample in one launch (csrc/dysample2.hip), bit-identical to the pair below; it reads
+            # and writes whole 16-byte channel vectors (check_view(need_vec_align) in ydbl_dysample2)
             wd = plan.const(w.reshape(8 * self.groups, x.c).to(plan.dtype))
             bd = plan.const(b)
             d = _lib.DySample2Desc(x.struct(), wd.data_ptr(), bd.data_ptr(), self.groups, y.struct(), _null_view(),
@@ -912,7 +924,6 @@ class DySample(nn.Module):
             return y
         off = plan.alloc(x.n, x.h, x.w, 8 * self.groups)
         emit_conv2d(plan, self.offset, x, off, w, b, what="DySample.offset")
-        y = out if out is not None else plan.alloc(x.n, 2 * x.h, 2 * x.w, x.c)
         d = _lib.DySampleDesc(x.struct(), off.struct(), self.groups, y.struct(), _null_view(), _null_view(), 0.0, 0.0)
         plan.launch("ydbl_dysample_ex", d, what="DySample.sample", keep=[d])
         plan.note_writer(y, d)  # a FullPAD_Tunnel on y becomes this launch's second output
@@ -936,7 +947,7 @@ class LSKblock(nn.Module):
         a1, a2 = emit_dw_pair(plan, self.conv0, self.conv_spatial, x, what="LSK.dw5+dw7d3")
         y = out if out is not None else plan.alloc(x.n, x.h, x.w, x.c)
         if (plan.dtype == torch.float16 and x.c in (256, 512) and not os.environ.get("YDBL_LSK_UNFUSED")
-                and x.cs % 8 == 0 and y.cs % 8 == 0 and y.base is not x.base):
+                and vec_aligned(x) and vec_aligned(y) and y.base is not x.base):
             # conv1 | conv2 + stats, then gate + conv + x * in two launches (csrc/lsk.hip)
             attn = plan.alloc(x.n, x.h, x.w, 2 * half)
             ws = plan.scratch(_lib.lib.ydbl_lsk_gate_workspace(x.n, x.h, x.w))

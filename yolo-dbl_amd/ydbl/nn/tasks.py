@@ -189,6 +189,58 @@ class DetectionModel(nn.Module):
     def nc(self):
         return self.model[-1].nc
 
+    MAX_FORWARD_SESSIONS = 2
+
+    def forward(self, x, *args, **kwargs):
+        """BaseModel.forward -> predict -> _predict_once (U/nn/tasks.py:109-172) with Detect's inference return
+        (U/nn/modules/head.py:108-118): ``(y, feats)``, y [B, 4+nc, A] = decoded xywh boxes (pixels) + class
+        scores (Detect._inference, head.py:143-181), feats = the per-level head maps cat(box, cls)
+        [B, 64+nc, H_i, W_i].  This is the call AutoBackend makes (U/nn/autobackend.py:503-528, ``self.model(im)``).
+
+        Runs the compiled HIP plan of x's (batch, h, w, dtype) on x's device -- forward + decode, no NMS --
+        replayed as a hipGraph; fp16 input takes the half path (AutoBackend fp16, autobackend.py:145-155).
+        BN is folded and the semantics are always inference (eval) ones; training / loss (dict input) and
+        augment / profile / visualize / embed are not on this path.  Returns fresh tensors (the plan's buffers
+        are reused by the next call).  CPU tensors raise: there is no CPU execution path."""
+        if isinstance(x, dict):
+            raise NotImplementedError("training loss (dict input) is outside the inference path")
+        if args or any(kwargs.get(k) for k in ("augment", "profile", "visualize", "embed")):
+            raise NotImplementedError("augment / profile / visualize / embed are outside the inference path")
+        if not isinstance(x, torch.Tensor) or x.ndim != 4:
+            raise TypeError("DetectionModel.forward takes a BCHW tensor")
+        if x.device.type != "cuda":
+            raise RuntimeError(f"ydbl runs on MI355X (gfx950) only: input on {x.device}, move it to a cuda device")
+        if x.dtype not in (torch.float32, torch.float16):
+            raise TypeError(f"input dtype {x.dtype}: float32 or float16 (half) expected")
+        if x.shape[1] != self.yaml["ch"]:
+            raise ValueError(f"input has {x.shape[1]} channels, the model {self.yaml['ch']}")
+        b, _, h, w = x.shape
+        s = self._forward_session(b, h, w, x.dtype == torch.float16, x.device)
+        s(x.float())
+        y = s.pred.to(x.dtype, copy=True)
+        feats = [f.contiguous() for f in s.feats()]
+        return y, feats
+
+    def _forward_session(self, b, h, w, half, device):
+        from ..engine.session import DetectSession
+
+        cache = self.__dict__.setdefault("_fwd_sessions", {})
+        key = (b, h, w, half, str(device))
+        s = cache.pop(key, None)
+        if s is None:
+            while len(cache) >= self.MAX_FORWARD_SESSIONS:
+                cache.pop(next(iter(cache)))
+            with torch.cuda.device(device):
+                s = DetectSession(self, b, h, w, torch.float16 if half else torch.float32, keep_pred=True, nms=False,
+                                  device=device)
+        cache[key] = s  # most recently used last
+        return s
+
+    def load_state_dict(self, *args, **kwargs):
+        """nn.Module.load_state_dict; compiled forward plans hold folded copies of the weights, so they go."""
+        self.__dict__.pop("_fwd_sessions", None)
+        return super().load_state_dict(*args, **kwargs)
+
     def fuse(self, verbose=False):
         """BN folding happens when a plan is compiled (exactly fuse_conv_and_bn's arithmetic); kept for API parity."""
         self._fused = True
