@@ -72,8 +72,8 @@ def _run(golden_dir, name, batch, mode, streams=1):
     return y64, meta, yg, dets, ref_dets
 
 
-@pytest.mark.parametrize("name,batch", [("n640", 32), ("n640", 2), ("s640", 2), ("s640", 32), ("l1280", 1),
-                                        ("l1280", 8), ("x640", 2)])
+@pytest.mark.parametrize("name,batch", [("n640", 32), ("n640", 2), ("s640", 16), ("s640", 32), ("l1280", 8),
+                                        ("x640", 2)])
 def test_e2e_fp32(golden_dir, name, batch):
     """x640 (DBL-x, not a BASELINE config): its trained-like fixture is ~50x worse conditioned than n/s/l (the
     reference fp32 path itself lands 0.36 px / 1e-3 from fp64), so the 2x rule is tight there: bs2 measured
@@ -88,7 +88,7 @@ def test_e2e_fp32(golden_dir, name, batch):
     checked, bad = class_agreement(yg, y64, tc)
     assert checked > 0 and bad == 0, (checked, bad)
     m = match_detections(ref_dets, dets, y64, meta["conf"], meta["iou"], tb, tc)
-    assert sum(len(d) for d in ref_dets) > 0
+    assert sum(len(d) for d in ref_dets) > 0  # (s640 images 0, 1 and l1280 image 0 have none at conf .25)
     # no more mismatches than the reference fp32 path's own under the same rule (0 on n640 / s640; the l1280
     # fixture's image 7 has one NMS decision that the reference fp32 path itself flips)
     assert len(m["mismatches"]) <= 2 * o32.get("det_mismatches", 0), m["mismatches"][:5]
@@ -97,7 +97,7 @@ def test_e2e_fp32(golden_dir, name, batch):
     assert m["borderline"] <= nb and m["pairs"] >= sum(len(d) for d in ref_dets) - nb, m
 
 
-@pytest.mark.parametrize("name,batch,streams", [("n640", 32, 1), ("n640", 32, 2), ("n640", 2, 1), ("s640", 8, 1),
+@pytest.mark.parametrize("name,batch,streams", [("n640", 32, 1), ("n640", 32, 2), ("n640", 2, 1), ("s640", 16, 1),
                                                 ("s640", 32, 2), ("l1280", 8, 1), ("x640", 8, 2)])
 def test_e2e_fp16(golden_dir, name, batch, streams):
     """streams=2: the bench's layout (two bs/2 sub-batch graphs replayed on two HIP streams)."""

@@ -36,33 +36,34 @@ struct ConvArgs {
   T* g0y; int g0ycs; int g0act;
 };
 
-// ---- in-launch hand-off of per-workgroup partials (MI355X_MICROARCH.md § inter-workgroup visibility, the sc1
-// slab recipe of cdna_hip_programming.md's split-K item): every workgroup stores its fp32 partials WRITE-THROUGH
-// (sc1 buffer stores), every storing wave drains them, one relaxed agent-scope ticket per workgroup; the
-// workgroup that draws the last ticket reads every slab with sc1 loads (L1 bypassed).  No __threadfence(): its
-// L2 write-back + invalidate in every workgroup cost 6x on a split-K conv.
+// ---- in-launch hand-off of activation tiles between workgroups (dsc3k_chain.hip; MI355X_MICROARCH.md
+// "Workgroup dispatch, XCD placement & inter-workgroup visibility", Valid forms, table row 1): EVERY store of a
+// handed-off byte is an sc1 (write-through) buffer store, every storing wave drains them (s_waitcnt vmcnt(0)),
+// a workgroup barrier, then ONE lane stores the tile's flag sc1; the consumer polls the flag with sc1 loads,
+// joins a workgroup barrier, and EVERY load of the handed-off bytes is an sc1 buffer load to registers (L1
+// bypassed).  No agent fences (1.7-3.5 us each).
+using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
 using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
-using gint = __attribute__((address_space(1))) int;
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t slab_rsrc(void* base, int bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+constexpr int HO_RECORDS = 0x40000000;    // bytes a hand-off view may span from its base pointer (1 GiB)
+constexpr unsigned HO_OOB = 0x7FFFFF00u;  // an offset past HO_RECORDS: the buffer load returns zeros
+constexpr int HO_SC1 = 16;                // buffer-instruction cache-policy bit sc1 (gfx940+)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ho_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, HO_RECORDS, 0x00020000);
 }
-__device__ __forceinline__ void slab_store(__amdgpu_buffer_rsrc_t r, int off, const f32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, 16);  // aux 16 = sc1
+__device__ __forceinline__ h8 ho_ld16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, HO_SC1));
 }
-__device__ __forceinline__ f32x4 slab_load(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+__device__ __forceinline__ h4 ho_ld8(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, HO_SC1));
 }
-// after this workgroup's slab stores: true (in every thread) when it drew the last of `nsplit` tickets
-__device__ __forceinline__ bool splitk_arrive(gint* cnt, int nsplit, int* lds_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // EVERY storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0)
-    *lds_flag = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nsplit - 1;
-  __syncthreads();
-  return *lds_flag != 0;
+__device__ __forceinline__ void ho_st8(__amdgpu_buffer_rsrc_t r, unsigned off, h4 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, HO_SC1);
 }
-__device__ __forceinline__ void splitk_reset(gint* cnt) {  // ready for the next launch (graph replay)
-  __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ int ho_ld32(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, HO_SC1);
+}
+__device__ __forceinline__ void ho_st32(__amdgpu_buffer_rsrc_t r, unsigned off, int v) {
+  __builtin_amdgcn_raw_buffer_store_b32((unsigned)v, r, off, 0, HO_SC1);
 }
 
 // ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------
@@ -111,6 +112,9 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s);
 // conv3x3.hip: fp16 3x3 stride-1 convs with Cin 32..128 and VGPR-resident weights.
 bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s);
 // dsc_lean.hip: one-round-trip DSConv / DWConv->Conv1x1 for the small-map shapes it is built for.
+// dsconv.hip: a ydbl_dsconv_desc's kernel arguments (fp16) and its descriptor rules (YDBL_OK or the error code).
+ConvArgs<_Float16> ds_args_f16(const ydbl_dsconv_desc* d);
+int ds_check(const ydbl_dsconv_desc* d);
 bool try_dsc_lean(const ConvArgs<_Float16>& a, const float* dww, const float* dwb, int dw_act, int k, int st, int dil,
                   hipStream_t s);
 

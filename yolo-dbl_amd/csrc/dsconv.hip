@@ -246,7 +246,7 @@ static int launch_ds(const ConvArgs<T>& a, const float* dww, const float* dwb, i
 }
 
 template <typename T>
-static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
+static ConvArgs<T> ds_args(const ydbl_dsconv_desc* d) {
   ConvArgs<T> a{};
   a.x = reinterpret_cast<const T*>(d->x.ptr);
   a.xcs = d->x.cs; a.N = d->x.n; a.H = d->x.h; a.W = d->x.w; a.Cin = d->x.c;
@@ -262,10 +262,25 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
     a.y3 = reinterpret_cast<T*>(d->tail_y.ptr); a.y3cs = d->tail_y.cs;
   }
   a.P = d->y.n * d->y.h * d->y.w;
-  if (d->g2_w) {  // trailing GEMM: only the lean kernel has it (ydbl.h: fp16, k 7 s 1, C 64 / 128)
+  if (d->g2_w) {
     a.g2w = reinterpret_cast<const T*>(d->g2_w); a.g2b = d->g2_b;
     a.g2x = reinterpret_cast<const T*>(d->g2_x.ptr); a.g2xcs = d->g2_x.cs;
     a.g2y = reinterpret_cast<T*>(d->g2_y.ptr); a.g2ycs = d->g2_y.cs; a.g2act = d->g2_act;
+  }
+  if (d->g0_w) {
+    a.g0w = reinterpret_cast<const T*>(d->g0_w); a.g0b = d->g0_b;
+    a.g0x = reinterpret_cast<const T*>(d->g0_x.ptr); a.g0xcs = d->g0_x.cs;
+    a.g0y = reinterpret_cast<T*>(d->g0_y.ptr); a.g0ycs = d->g0_y.cs; a.g0act = d->g0_act;
+  }
+  return a;
+}
+
+ConvArgs<_Float16> ds_args_f16(const ydbl_dsconv_desc* d) { return ds_args<_Float16>(d); }
+
+template <typename T>
+static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
+  const ConvArgs<T> a = ds_args<T>(d);
+  if (d->g2_w) {  // trailing GEMM: only the lean kernel has it (ydbl.h: fp16, k 7 s 1, C 64 / 128)
     if constexpr (sizeof(T) == 2) {
       if (d->k == 7 && d->stride == 1 && d->dil == 1 &&
           try_dsc_lean(a, d->dw_w, d->dw_bias, d->dw_act, 7, 1, 1, s))
@@ -274,9 +289,6 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
     return fail(YDBL_EINVAL, "dsconv: the trailing GEMM (g2) needs fp16, k 7 stride 1, C 64 or 128 (lean kernel)");
   }
   if (d->g0_w) {  // leading 1x1: only the lean kernel has it (ydbl.h: fp16, k 3 s 1, C 64, g0_y 128)
-    a.g0w = reinterpret_cast<const T*>(d->g0_w); a.g0b = d->g0_b;
-    a.g0x = reinterpret_cast<const T*>(d->g0_x.ptr); a.g0xcs = d->g0_x.cs;
-    a.g0y = reinterpret_cast<T*>(d->g0_y.ptr); a.g0ycs = d->g0_y.cs; a.g0act = d->g0_act;
     if constexpr (sizeof(T) == 2) {
       if (d->k == 3 && d->stride == 1 && d->dil == 1 &&
           try_dsc_lean(a, d->dw_w, d->dw_bias, d->dw_act, 3, 1, 1, s))
@@ -291,11 +303,8 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
   return fail(YDBL_EINVAL, "dsconv: supported (k, stride, dil): (3,1,1) (3,2,1) (5,1,1) (7,1,1)");
 }
 
-}  // namespace ydbl
-
-using namespace ydbl;
-
-extern "C" int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream) {
+// The descriptor rules of ydbl_dsconv_nhwc (include/ydbl.h); also applied to every stage of ydbl_dsc3k_chain.
+int ds_check(const ydbl_dsconv_desc* d) {
   if (!d) return fail(YDBL_EINVAL, "dsconv: null descriptor");
   if (check_view(&d->x, "dsconv.x", true) || check_view(&d->y, "dsconv.y", false)) return YDBL_EINVAL;
   if (d->x.dtype != d->y.dtype || d->x.n != d->y.n) return fail(YDBL_EINVAL, "dsconv: x/y mismatch");
@@ -337,6 +346,15 @@ extern "C" int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream) {
         d->tail_y.n != d->y.n || d->tail_y.h != d->y.h || d->tail_y.w != d->y.w)
       return fail(YDBL_EINVAL, "dsconv: tail needs y.c 64, 1 <= tail_n <= 4, tail_y [n,h,w,tail_n] of y's dtype, no residual");
   }
+  return YDBL_OK;
+}
+
+}  // namespace ydbl
+
+using namespace ydbl;
+
+extern "C" int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream) {
+  if (const int rc = ds_check(d)) return rc;
   const hipStream_t s = as_stream(stream);
   return d->x.dtype == YDBL_F16 ? run_ds<_Float16>(d, s) : run_ds<float>(d, s);
 }
