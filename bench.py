@@ -160,18 +160,6 @@ def hg_fused_traffic(step, elsize):
     return 2 * n * dd * elsize, 2.0 * n * (dd * dd + 3 * e * dd) + 2.0 * d.x.n * e * dd * (2 * dd + 2 * dd)
 
 
-def chain_traffic(step, elsize):
-    """ydbl_dsc3k_chain: its four DSConv stages' bytes / FLOPs (each stage's input read and output written: the
-    intermediates still make the round trip through the memory hierarchy, in-launch)."""
-    d = step.args[0]
-    tot = [0.0, 0.0]
-    for i in range(4):
-        b, f = dsconv_traffic(type("S", (), {"args": (d.st[i],)})(), elsize)
-        tot[0] += b
-        tot[1] += f
-    return tot[0], tot[1]
-
-
 def lsk_traffic(step, elsize):
     """ydbl_lsk_attn: a1, a2 read, attn = conv1(a1) | conv2(a2) written (+ per-pixel stats, left out);
     ydbl_lsk_out: attn and x read, y = x * conv(gate(attn)) written (LSKA.py:43-52)."""
@@ -186,7 +174,7 @@ TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("d
            "ydbl_dysample2": ("dysample", dysample2_traffic), "ydbl_hg_fused": ("hypergraph", hg_fused_traffic),
            "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
            "ydbl_dysample_ex": ("dysample", dysample_traffic), "ydbl_lsk_attn": ("lsk", lsk_traffic),
-           "ydbl_lsk_out": ("lsk", lsk_traffic), "ydbl_dsc3k_chain": ("dsc3k_chain", chain_traffic)}
+           "ydbl_lsk_out": ("lsk", lsk_traffic)}
 
 
 def roofline(session, dtype_name, key=None, step_ms=None):

@@ -41,8 +41,6 @@
  *   ydbl_dysample2         <- DySample.forward DySample.py:63-81 (offset conv + sample, one launch)
  *   ydbl_lsk_gate          <- LSKblock.forward LSKA.py:40-52 (mean/max, 7x7 squeeze, sigmoid gating)
  *   ydbl_lsk_attn/_out     <- LSKblock.forward LSKA.py:43-52 (conv1 | conv2 + stats; gate + conv + x *)
- *   ydbl_dsc3k_chain       <- DSC3k block.py:1447-1503 (its DSBottlenecks :1408-1444, C3's cv1/cv2/cv3
- *                             :259-273) as one launch of the four DSConv stages
  *   ydbl_hg_*              <- AdaHyperedgeGen/AdaHGConv block.py:1627-1708 (ydbl_hg_fused: the whole
  *                             AdaHGConv incl. pre_head_proj block.py:1645, one call)
  *   ydbl_detect_decode     <- Detect._inference head.py:143-181 + DFL block.py:79-83 +
@@ -146,23 +144,6 @@ typedef struct {
   int32_t g0_act;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
-
-/* DSC3k (block.py:1447-1503 with its two DSBottlenecks block.py:1408-1444, DSC3k2's inner block) after its input
- * as ONE launch: the four ydbl_dsconv_nhwc launches the plan builder emits for it, as stages
- *   st[0] k3 with the leading 1x1 (g0: C3's merged cv2 | cv1), st[1] k7 + residual ADD (r = st[0].x = cv1),
- *   st[2] k3, st[3] k7 + residual ADD (r = st[1].y) with the trailing GEMM (g2: cv3 over [y ; cv2]),
- * each stage's x being the previous stage's y; every stage obeys ydbl_dsconv_nhwc's rules.  Built for fp16,
- * 64 channels, stride 1.  Bit-identical to the four launches.  ctrl: ydbl_dsc3k_chain_workspace(n, h, w) bytes,
- * ZEROED once before the first call and left by each call ready for the next (graph replays need no reset).
- * The stages overlap inside the launch through per-tile flags (csrc/dsc3k_chain.hip); ydbl_dsc3k_chain_status
- * reads back (synchronising the stream) whether any wait timed out since ctrl was zeroed. */
-typedef struct {
-  ydbl_dsconv_desc st[4];
-  void* ctrl;
-} ydbl_dsc3k_chain_desc;
-int64_t ydbl_dsc3k_chain_workspace(int32_t n, int32_t h, int32_t w);
-int ydbl_dsc3k_chain(const ydbl_dsc3k_chain_desc* d, void* stream);
-int ydbl_dsc3k_chain_status(const void* ctrl, void* stream);
 
 /* Depthwise convolution (groups = C), fp32 arithmetic.
  * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).

@@ -33,7 +33,6 @@ FAMILIES = {  # family -> (kernel-name keys, FETCH_SIZE multiplier)
     "hypergraph": (("hg_", "hg3_"), 2),
     "dysample": (("dysample_kernel", "dysample2_kernel"), 2),
     "lsk": (("lsk_attn_kernel", "lsk_out_kernel"), 2),
-    "dsc3k_chain": (("dsc3k_chain_kernel",), 2),
     "decode": (("decode_kernel",), 1),
     "nms": (("nms_kernel",), 1),
 }

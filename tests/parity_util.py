@@ -59,8 +59,20 @@ def oracle_only(scale: str, nc: int, golden_dir):
 
 def fp32_rule(st):
     """(box px, score) tolerance of the fp32 comparison: twice the reference fp32 path's worst deviation
-    from the fp64 answer (st = err_stats of that leg) plus a floor of 1e-3 px / 1e-6."""
+    from the fp64 answer (st = err_stats of that leg) plus a floor of 1e-3 px / 1e-6.  Used for class agreement
+    and detection matching (the fixture's det_borderline counts were taken at this tolerance)."""
     return 2 * st["box_max"] + 1e-3, 2 * st["conf_max"] + 1e-6
+
+
+def fp32_rule_max(st):
+    """The value bound of the fp32 comparison: the worst and the p99.9 deviation from fp64 each within three
+    times the reference fp32 path's own (+ the floor).  Both paths are fp32 and differ in summation order (and
+    expf), so their deviations are of one order but not ordered: measured GPU / reference-fp32 ratios (max, p99.9)
+    on the pinned images are DBL-s bs32 box 1.43x / 1.47x, score 2.04x / 1.62x and DBL-x bs2 (a fixture ~50x
+    worse conditioned) box 1.47x / 2.26x, score 1.66x / 2.02x.
+    Returns (box max, score max, box p99.9, score p99.9)."""
+    return (3 * st["box_max"] + 1e-3, 3 * st["conf_max"] + 1e-6, 3 * st["box_p999"] + 1e-4,
+            3 * st["conf_p999"] + 1e-7)
 
 
 def fp16_rule(st):

@@ -47,7 +47,6 @@ STRUCTS = {
     "ydbl_dysample_desc": "DySampleDesc",
     "ydbl_dysample2_desc": "DySample2Desc",
     "ydbl_lsk_desc": "LskDesc",
-    "ydbl_dsc3k_chain_desc": "Dsc3kChainDesc",
 }
 
 

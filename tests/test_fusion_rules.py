@@ -49,18 +49,3 @@ def test_cv3_fusable_small_map_rule_for_128_channels(monkeypatch):
     m = M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)
     assert m._cv3_fusable(plan, _x(16, 128, 20, 20))      # 16 * 3 * 3 = 144 8x8 tiles <= 160
     assert not m._cv3_fusable(plan, _x(64, 128, 40, 40))  # DBL-s bs64: 1600 tiles -> chunked kernel
-
-
-def test_dsc3k_chain_rule(monkeypatch):
-    """DSC3k with the leading + trailing GEMMs and two k3/k7 DSBottlenecks at c_ 64 runs as one ydbl_dsc3k_chain
-    launch (csrc/dsc3k_chain.hip); other shapes keep the separate launches."""
-    monkeypatch.delenv("YDBL_DSC3K_CHAIN", raising=False)
-    plan = NS(dtype=torch.float16)
-    assert M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=7)._chain_ok(plan, _x(16, 64))
-    assert not M.DSC3k(64, 64, 1, True, e=1.0, k1=3, k2=7)._chain_ok(plan, _x(16, 64))  # one bottleneck
-    assert not M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=5)._chain_ok(plan, _x(16, 64))
-    assert M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)._chain_ok(plan, _x(16, 128, 20, 20))
-    assert not M.DSC3k(256, 256, 2, True, e=1.0, k1=3, k2=7)._chain_ok(plan, _x(16, 256, 20, 20))
-    assert not M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=7)._chain_ok(NS(dtype=torch.float32), _x(16, 64))
-    monkeypatch.setenv("YDBL_DSC3K_CHAIN", "0")
-    assert not M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=7)._chain_ok(plan, _x(16, 64))

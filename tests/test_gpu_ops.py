@@ -1219,54 +1219,3 @@ def test_lsk_fused_bit_identical(c, shape, sliced, monkeypatch):
     with torch.no_grad():
         ref = o(x)
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
-
-
-@pytest.mark.parametrize("shape,sliced,replays", [((16, 64, 40, 40), False, 3), ((32, 64, 40, 40), True, 2),
-                                                   ((3, 64, 20, 36), False, 2), ((1, 64, 13, 9), True, 1),
-                                                   ((16, 128, 20, 20), False, 3), ((2, 128, 11, 19), True, 2)])
-def test_dsc3k_chain_bit_identical(shape, sliced, replays, monkeypatch):
-    """DSC3k (c_ 64, two k3/k7 DSBottlenecks, leading cv2 | cv1 and trailing cv3 GEMMs) as ONE ydbl_dsc3k_chain
-    launch == its four ydbl_dsconv_nhwc launches, bit for bit (same tile function, stages overlapped through
-    per-tile flags), with every intermediate (cv2 | cv1, both bottleneck outputs) equal too; replayed several
-    times (the control block's epoch carries over, no reset launch); no stage wait timed out."""
-    from oracle import model as om
-    from ydbl.nn import modules as M
-    from ydbl.utils.synthetic import trained_like_
-
-    c = shape[1]
-    torch.manual_seed(shape[0] + shape[2])
-    o = trained_like_(om.DSC3k(c, c, 2, True, e=1.0, k1=3, k2=7), seed=11).eval()
-    xs = [torch.randn(*shape) for _ in range(replays)]
-    res = {}
-    monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
-    monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
-    monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
-    for chain in ("1", "0"):
-        monkeypatch.setenv("YDBL_DSC3K_CHAIN", chain)
-        pm = M.DSC3k(c, c, 2, True, e=1.0, k1=3, k2=7)
-        pm.load_state_dict(o.state_dict())
-        plan = _plan(torch.float16)
-        xv = _tv_from_nchw(plan, xs[0])
-        ybuf = plan.alloc(shape[0], shape[2], shape[3], c + (24 if sliced else 0))
-        yv = ybuf.cslice(8, c) if sliced else ybuf
-        pm.emit(plan, xv, yv)
-        kinds = [st.fn.__name__ for st in plan.steps]
-        assert ("ydbl_dsc3k_chain" in kinds) == (chain == "1"), kinds
-        outs = []
-        for x in xs:
-            xv.torch().copy_(x.permute(0, 2, 3, 1).to(xv.dtype))
-            _run(plan)
-            # the output and every buffer the plan wrote (intermediates included)
-            outs.append([yv.nchw().float().cpu()] + [b.float().cpu().clone() for b in plan.buffers
-                                                     if b.dtype == torch.float16 and b.data_ptr() != xv.base.data_ptr()
-                                                     and b.data_ptr() != ybuf.base.data_ptr()])
-        if chain == "1":
-            assert plan.chain_errors() == 0
-            assert len(plan.steps) == 1
-        res[chain] = outs
-    for a, b in zip(res["1"], res["0"]):
-        assert torch.equal(a[0], b[0]), (a[0] - b[0]).abs().max()
-        assert len(a) == len(b) and all(torch.equal(u, v) for u, v in zip(a[1:], b[1:]))
-    with torch.no_grad():
-        ref = o(xs[-1])
-    torch.testing.assert_close(res["1"][-1][0], ref, rtol=3e-2, atol=3e-2)

@@ -75,6 +75,17 @@ __device__ __forceinline__ typename Vec<T>::type vload_sel(const T* p, const T* 
   typename Vec<T>::type v = vload(ok ? p : safe);
   return ok ? v : vzero<T>();
 }
+// The same split in two for prefetch pipelines: the load from the clamped address now, the zero select where
+// the value is consumed (a select next to its load makes the compiler wait for that load right there: one full
+// memory round trip per prefetched vector instead of one per pipeline stage).
+template <typename T>
+__device__ __forceinline__ typename Vec<T>::type vload_clamped(const T* p, const T* safe, bool ok) {
+  return vload(ok ? p : safe);
+}
+template <typename V>
+__device__ __forceinline__ V vsel(const V& v, bool ok) {
+  return ok ? v : V{};
+}
 
 // Load/store VEC elements as fp32.
 template <typename T, int N>

@@ -31,12 +31,13 @@ __device__ __forceinline__ int swz(int row, int kv) {
   else return row * 4 + (kv ^ (((row >> 2) & 1) << 1));
 }
 
-template <typename T, int BM, int BN, int WM, int WN, bool POINTWISE, bool Q8>
+template <typename T, int BM, int BN, int WM, int WN, bool POINTWISE, bool Q8, int PF = 1>
 __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "tile config");
+  static_assert(PF >= 1 && PF <= 4, "prefetch depth");
   constexpr int A_IT = (BN * 4 + 255) / 256, B_IT = (BM * 4 + 255) / 256;
   using vec = typename Vec<T>::type;
   using opv = typename Op<T, Q8>::lds;
@@ -77,10 +78,14 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
     biy[it] = oy * p.S - p.PAD;
     bix[it] = ox * p.S - p.PAD;
   }
-  opv ra[A_IT];
-  vec rb[B_IT];
+  // PF register slots: step s lives in slot s % PF from its load (issued PF steps before it is computed,
+  // so PF - 1 steps of MFMA work cover its latency) until its LDS store
+  opv ra[PF][A_IT];
+  vec rb[PF][B_IT];
+  bool rok[PF][B_IT], aok[PF][A_IT];
   // k-walk state: every staging vector of this thread has k-vector tid&3, so one (ky, kx, ci)
-  // cursor serves all of them; it advances by BK per step with no integer division.
+  // cursor serves all of them; it advances by BK per step with no integer division (loads are issued
+  // in step order, so one cursor serves the prefetch ring too).
   int cur_ci = (tid & 3) * VEC, cur_kx = 0, cur_ky = 0;
   if constexpr (!POINTWISE) {
     const int tap = cur_ci / p.Cin;
@@ -97,35 +102,41 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
       }
     }
   };
-  auto load_step = [&](int ks) {
-    // every load is unconditional (clamped address) and masked afterwards: no branch per load
+  // raw loads now, zero selects at the LDS store (vload_clamped): a slot's loads stay in flight until then
+  // Steps past the end (the ring's tail) load nothing: k >= K masks B, k >= KPAD masks A (clamped addresses).
+  auto load_step = [&](int ks, opv (&a)[A_IT], bool (&aok)[A_IT], vec (&b)[B_IT], bool (&bok)[B_IT]) {
 #pragma unroll
-    for (int it = 0; it < A_IT; ++it) ra[it] = load_wop<T, Q8>(p.w, arow[it] + ks * BK, aval[it]);
+    for (int it = 0; it < A_IT; ++it) {
+      aok[it] = aval[it] && ks * BK < p.KPAD;
+      a[it] = load_wop_raw<T, Q8>(p.w, arow[it] + ks * BK, aok[it]);
+    }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int v = tid + it * 256;
       const int k = ks * BK + (v & 3) * VEC;
       const bool kin = k < p.K;
       if constexpr (POINTWISE) {
-        rb[it] = vload_sel(p.x + bpix[it] * p.xcs + k, p.x, bval[it] && kin);
+        bok[it] = bval[it] && kin;
+        b[it] = vload_clamped(p.x + bpix[it] * p.xcs + k, p.x, bok[it]);
       } else {
         const int iy = biy[it] + cur_ky * p.DIL, ix = bix[it] + cur_kx * p.DIL;
-        const bool ok = bval[it] && kin && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        rb[it] = vload_sel(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + cur_ci, p.x, ok);
+        bok[it] = bval[it] && kin && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        b[it] = vload_clamped(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + cur_ci, p.x, bok[it]);
       }
     }
     advance();
   };
-  auto store_step = [&](int buf) {
+  auto store_step = [&](int buf, const opv (&a)[A_IT], const bool (&aok)[A_IT], const vec (&b)[B_IT],
+                        const bool (&bok)[B_IT]) {
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int v = tid + it * 256;
-      if (v < BN * 4) sA[buf][swz<Q8>(v >> 2, v & 3)] = ra[it];
+      if (v < BN * 4) sA[buf][swz<Q8>(v >> 2, v & 3)] = vsel(a[it], aok[it]);
     }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int v = tid + it * 256;
-      if (v < BM * 4) sB[buf][swz<Q8>(v >> 2, v & 3)] = to_op<T, Q8>(rb[it], p.qs);
+      if (v < BM * 4) sB[buf][swz<Q8>(v >> 2, v & 3)] = to_op<T, Q8>(vsel(b[it], bok[it]), p.qs);
     }
   };
 
@@ -136,23 +147,33 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nsteps = (p.K + BK - 1) / BK;
-  load_step(0);
-  store_step(0);
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_step(u, ra[u], aok[u], rb[u], rok[u]);
+  store_step(0, ra[0], aok[0], rb[0], rok[0]);
   __syncthreads();
-  for (int ks = 0; ks < nsteps; ++ks) {
-    const int buf = ks & 1;
-    if (ks + 1 < nsteps) load_step(ks + 1);
-    opv af[TN], bf[TM];
+  // The loads are unconditional (past the end they are masked no-ops), so the waitcnt pass sees one fixed
+  // order of outstanding loads and waits only for the slot being stored.
+  for (int k0 = 0; k0 < nsteps; k0 += PF) {
 #pragma unroll
-    for (int i = 0; i < TN; ++i) af[i] = sA[buf][swz<Q8>(wn * TN * 16 + i * 16 + r16, g)];
+    for (int u = 0; u < PF; ++u) {
+      const int ks = k0 + u;
+      if (PF > 1 || ks + PF < nsteps) load_step(ks + PF, ra[u], aok[u], rb[u], rok[u]);  // slot u's step is in LDS
+      if (ks < nsteps) {  // uniform
+        const int buf = ks & 1;
+        opv af[TN], bf[TM];
 #pragma unroll
-    for (int j = 0; j < TM; ++j) bf[j] = sB[buf][swz<Q8>(wm * TM * 16 + j * 16 + r16, g)];
+        for (int i = 0; i < TN; ++i) af[i] = sA[buf][swz<Q8>(wn * TN * 16 + i * 16 + r16, g)];
 #pragma unroll
-    for (int i = 0; i < TN; ++i)
+        for (int j = 0; j < TM; ++j) bf[j] = sB[buf][swz<Q8>(wm * TM * 16 + j * 16 + r16, g)];
 #pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
-    if (ks + 1 < nsteps) store_step(buf ^ 1);
-    __syncthreads();
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
+        const int nx = (u + 1) % PF;
+        if (ks + 1 < nsteps) store_step(buf ^ 1, ra[nx], aok[nx], rb[nx], rok[nx]);
+        __syncthreads();
+      }
+    }
   }
 
   // ---- epilogue
@@ -331,7 +352,7 @@ static bool try_tile(const ConvArgs<T>& a, int kh, hipStream_t s) {
 // tiles are summed through LDS in fixed wave order before the fused epilogue.
 // LDS rows are 16 vectors (4*BK elements), slot-swizzled with (kv ^ row) so both the staging
 // stores and the 16x16 fragment reads are bank-conflict-free.
-template <typename T, int BM, int BN, bool POINTWISE, bool Q8>
+template <typename T, int BM, int BN, bool POINTWISE, bool Q8, int PF = 1>
 __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;    // per wave
@@ -383,21 +404,25 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     cur_ky = tap / p.KW;
     cur_kx = tap - cur_ky * p.KW;
   }
-  opv ra[A_IT];
-  vec rb[B_IT];
-  auto load_step = [&](int kb) {
+  // PF register slots as in conv_igemm_kernel: raw loads, zero selects at the LDS store, loads unconditional
+  opv ra[PF][A_IT];
+  vec rb[PF][B_IT];
+  bool aok[PF], bok[PF][B_IT];
+  auto load_step = [&](int kb, opv (&a)[A_IT], bool& ak, vec (&b)[B_IT], bool (&bk)[B_IT]) {
     const int k = kb * BKB + kv * VEC;
     const bool kin = k < p.K;
+    ak = kin;
 #pragma unroll
-    for (int it = 0; it < A_IT; ++it) ra[it] = load_wop<T, Q8>(p.w, arow[it] + kb * BKB, aval[it] && kin);
+    for (int it = 0; it < A_IT; ++it) a[it] = load_wop_raw<T, Q8>(p.w, arow[it] + kb * BKB, aval[it] && kin);
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       if constexpr (POINTWISE) {
-        rb[it] = vload_sel(p.x + bpix[it] * p.xcs + k, p.x, bval[it] && kin);
+        bk[it] = bval[it] && kin;
+        b[it] = vload_clamped(p.x + bpix[it] * p.xcs + k, p.x, bk[it]);
       } else {
         const int iy = biy[it] + cur_ky * p.DIL, ix = bix[it] + cur_kx * p.DIL;
-        const bool ok = bval[it] && kin && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-        rb[it] = vload_sel(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + cur_ci, p.x, ok);
+        bk[it] = bval[it] && kin && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        b[it] = vload_clamped(p.x + ((int64_t)(bb[it] * p.H + iy) * p.W + ix) * p.xcs + cur_ci, p.x, bk[it]);
       }
     }
     if constexpr (!POINTWISE) {
@@ -408,16 +433,16 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
       }
     }
   };
-  auto store_step = [&](int buf) {
+  auto store_step = [&](int buf, const opv (&a)[A_IT], bool ak, const vec (&b)[B_IT], const bool (&bk)[B_IT]) {
 #pragma unroll
     for (int it = 0; it < A_IT; ++it) {
       const int row = (tid + it * 256) >> 4;
-      sA[buf * BN * 16 + row * 16 + (kv ^ (row & 15))] = ra[it];
+      sA[buf * BN * 16 + row * 16 + (kv ^ (row & 15))] = vsel(a[it], aval[it] && ak);
     }
 #pragma unroll
     for (int it = 0; it < B_IT; ++it) {
       const int row = (tid + it * 256) >> 4;
-      sB[buf * BM * 16 + row * 16 + (kv ^ (row & 15))] = to_op<T, Q8>(rb[it], p.qs);
+      sB[buf * BM * 16 + row * 16 + (kv ^ (row & 15))] = to_op<T, Q8>(vsel(b[it], bk[it]), p.qs);
     }
   };
 
@@ -428,30 +453,38 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nsteps = (p.K + BKB - 1) / BKB;
-  load_step(0);
-  store_step(0);
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load_step(u, ra[u], aok[u], rb[u], bok[u]);
+  store_step(0, ra[0], aok[0], rb[0], bok[0]);
   __syncthreads();
   const int myk = wave * 4 + g;  // k-vector this lane reads inside a block step
-  for (int kb = 0; kb < nsteps; ++kb) {
-    const int buf = kb & 1;
-    if (kb + 1 < nsteps) load_step(kb + 1);
-    opv af[TN], bf[TM];
+  for (int k0 = 0; k0 < nsteps; k0 += PF) {
 #pragma unroll
-    for (int i = 0; i < TN; ++i) {
-      const int row = i * 16 + r16;
-      af[i] = sA[buf * BN * 16 + row * 16 + (myk ^ (row & 15))];
+    for (int u = 0; u < PF; ++u) {
+      const int kb = k0 + u;
+      if (PF > 1 || kb + PF < nsteps) load_step(kb + PF, ra[u], aok[u], rb[u], bok[u]);
+      if (kb < nsteps) {  // uniform
+        const int buf = kb & 1;
+        opv af[TN], bf[TM];
+#pragma unroll
+        for (int i = 0; i < TN; ++i) {
+          const int row = i * 16 + r16;
+          af[i] = sA[buf * BN * 16 + row * 16 + (myk ^ (row & 15))];
+        }
+#pragma unroll
+        for (int j = 0; j < TM; ++j) {
+          const int row = j * 16 + r16;
+          bf[j] = sB[buf * BM * 16 + row * 16 + (myk ^ (row & 15))];
+        }
+#pragma unroll
+        for (int i = 0; i < TN; ++i)
+#pragma unroll
+          for (int j = 0; j < TM; ++j) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
+        const int nx = (u + 1) % PF;
+        if (kb + 1 < nsteps) store_step(buf ^ 1, ra[nx], aok[nx], rb[nx], bok[nx]);
+        __syncthreads();
+      }
     }
-#pragma unroll
-    for (int j = 0; j < TM; ++j) {
-      const int row = j * 16 + r16;
-      bf[j] = sB[buf * BM * 16 + row * 16 + (myk ^ (row & 15))];
-    }
-#pragma unroll
-    for (int i = 0; i < TN; ++i)
-#pragma unroll
-      for (int j = 0; j < TM; ++j) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
-    if (kb + 1 < nsteps) store_step(buf ^ 1);
-    __syncthreads();
   }
 
   // cross-wave reduction: partial tile (i, j) of wave w at red[((w * TN + i) * TM + j) * 64 + lane]
@@ -477,13 +510,16 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   }
 }
 
+// Two k-block steps in flight (kbench bs16: 256->64 3x3 @20^2 18.8 -> 17.4 us; three or four: no better)
+constexpr int WSK_PF = 2;
+
 template <typename T, bool Q8, int BM, int BN>
 static void launch_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
   if (pointwise)
-    conv_wsk_kernel<T, BM, BN, true, Q8><<<grid, 256, 0, s>>>(a);
+    conv_wsk_kernel<T, BM, BN, true, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
   else
-    conv_wsk_kernel<T, BM, BN, false, Q8><<<grid, 256, 0, s>>>(a);
+    conv_wsk_kernel<T, BM, BN, false, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
 }
 
 // Wave-split-K where the block-tiled GEMM runs out of parallelism or k-depth per barrier:
@@ -509,6 +545,9 @@ static bool try_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   return true;
 }
 
+// One k-step in flight: with the zero selects at the LDS store the loads of step s+1 overlap step s's MFMAs
+// (kbench bs16: 512->128 1x1 @40^2 16.9 -> 13.2 us, 128->64 @80^2 19.4 -> 11.1); deeper rings (2-4 steps,
+// the kernel's PF parameter) measured slower on every 1x1 shape (512->128: 13.4 / 14.6 / 14.2 us).
 template <typename T, bool Q8, int BM, int BN, int WM, int WN>
 static void launch_igemm(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));

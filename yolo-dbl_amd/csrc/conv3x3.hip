@@ -86,21 +86,25 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     wok[it] = co < p.Cout;
     wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
+  // raw loads, zero selects at the LDS store (vload_clamped): the next chunk stays in flight during the MFMAs;
+  // the load is unconditional (past the last chunk it is a masked no-op) so the waitcnt pass sees one order
   vec xr[XIT];
   opv wr[WIT];
+  bool cok = true;
   auto load_chunk = [&](int c0) {
+    cok = c0 < p.Cin;
 #pragma unroll
-    for (int it = 0; it < XIT; ++it) xr[it] = vload_sel(xsrc[it] + c0, p.x, xok[it]);
+    for (int it = 0; it < XIT; ++it) xr[it] = vload_clamped(xsrc[it] + c0, p.x, xok[it] && cok);
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) wr[it] = load_wop<T, Q8>(p.w, wsrc[it] + c0, wok[it]);
+    for (int it = 0; it < WIT; ++it) wr[it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0, wok[it] && cok);
   };
   auto store_chunk = [&]() {
 #pragma unroll
     for (int it = 0; it < XIT; ++it)
-      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(xr[it], p.qs);
+      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
 #pragma unroll
     for (int it = 0; it < WIT; ++it)
-      if (it * 256 + tid < WV) s_w[it * 256 + tid] = wr[it];
+      if (it * 256 + tid < WV) s_w[it * 256 + tid] = vsel(wr[it], wok[it] && cok);
   };
 
   f32x4 acc[NTN][TMW];
@@ -115,7 +119,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   store_chunk();
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
-    if (ch + 1 < nchunks) load_chunk((ch + 1) * BK);
+    load_chunk((ch + 1) * BK);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap % 3;

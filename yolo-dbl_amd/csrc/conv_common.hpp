@@ -36,36 +36,6 @@ struct ConvArgs {
   T* g0y; int g0ycs; int g0act;
 };
 
-// ---- in-launch hand-off of activation tiles between workgroups (dsc3k_chain.hip; MI355X_MICROARCH.md
-// "Workgroup dispatch, XCD placement & inter-workgroup visibility", Valid forms, table row 1): EVERY store of a
-// handed-off byte is an sc1 (write-through) buffer store, every storing wave drains them (s_waitcnt vmcnt(0)),
-// a workgroup barrier, then ONE lane stores the tile's flag sc1; the consumer polls the flag with sc1 loads,
-// joins a workgroup barrier, and EVERY load of the handed-off bytes is an sc1 buffer load to registers (L1
-// bypassed).  No agent fences (1.7-3.5 us each).
-using u32x2 = __attribute__((ext_vector_type(2))) unsigned int;
-using u32x4 = __attribute__((ext_vector_type(4))) unsigned int;
-constexpr int HO_RECORDS = 0x40000000;    // bytes a hand-off view may span from its base pointer (1 GiB)
-constexpr unsigned HO_OOB = 0x7FFFFF00u;  // an offset past HO_RECORDS: the buffer load returns zeros
-constexpr int HO_SC1 = 16;                // buffer-instruction cache-policy bit sc1 (gfx940+)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ho_rsrc(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, HO_RECORDS, 0x00020000);
-}
-__device__ __forceinline__ h8 ho_ld16(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, HO_SC1));
-}
-__device__ __forceinline__ h4 ho_ld8(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return __builtin_bit_cast(h4, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, HO_SC1));
-}
-__device__ __forceinline__ void ho_st8(__amdgpu_buffer_rsrc_t r, unsigned off, h4 v) {
-  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), r, off, 0, HO_SC1);
-}
-__device__ __forceinline__ int ho_ld32(__amdgpu_buffer_rsrc_t r, unsigned off) {
-  return (int)__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, HO_SC1);
-}
-__device__ __forceinline__ void ho_st32(__amdgpu_buffer_rsrc_t r, unsigned off, int v) {
-  __builtin_amdgcn_raw_buffer_store_b32((unsigned)v, r, off, 0, HO_SC1);
-}
-
 // ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------
 template <typename T, bool Q8> struct Op {
   using lds = typename Vec<T>::type;
@@ -93,7 +63,16 @@ __device__ __forceinline__ typename Op<T, Q8>::lds to_op(const typename Vec<T>::
 }
 
 // weight (A operand) load of one k-vector: VEC elements of T, or 8 e4m3 bytes at the same
-// element offset (the fp8 matrix is [Cout][KPAD] bytes)
+// element offset (the fp8 matrix is [Cout][KPAD] bytes); load_wop_raw leaves the zero select to the consumer
+template <typename T, bool Q8>
+__device__ __forceinline__ typename Op<T, Q8>::lds load_wop_raw(const T* w, int64_t off, bool ok) {
+  if constexpr (Q8) {
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(w);
+    return *reinterpret_cast<const uint64_t*>(b + (ok ? off : 0));
+  } else {
+    return vload_clamped(w + off, w, ok);
+  }
+}
 template <typename T, bool Q8>
 __device__ __forceinline__ typename Op<T, Q8>::lds load_wop(const T* w, int64_t off, bool ok) {
   if constexpr (Q8) {

@@ -28,7 +28,7 @@ __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, c
                                                           const float* __restrict__ dwb, int dw_act, int tiles_x,
                                                           int tiles_y, int ntiles) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LeanLds<C, CO, K, S, TH, TW, NT, TG, PRE>::BYTES];
-  lean_tile<C, CO, K, S, TH, TW, NT, TG, TAIL, PRE, false>(p, dww, dwb, dw_act, xcd_remap(blockIdx.x, ntiles), tiles_x,
+  lean_tile<C, CO, K, S, TH, TW, NT, TG, TAIL, PRE>(p, dww, dwb, dw_act, xcd_remap(blockIdx.x, ntiles), tiles_x,
                                                           tiles_y, smem);
 }
 

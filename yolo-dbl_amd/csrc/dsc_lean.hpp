@@ -1,5 +1,4 @@
-// The lean DSConv tile (dsc_lean.hip) as a device function, shared by the standalone lean kernel and the
-// DSC3k chain kernel (dsc3k_chain.hip).  See dsc_lean.hip for the design.
+// The lean DSConv tile (dsc_lean.hip) as a device function.  See dsc_lean.hip for the design.
 #pragma once
 #include "conv_common.hpp"
 
@@ -7,7 +6,7 @@ namespace ydbl {
 
 __device__ __forceinline__ int lean_bswz(int row, int kv) { return row * 4 + (kv ^ (((row >> 2) & 1) << 1)); }
 
-// LDS carve-up of one lean tile (shared by the standalone kernel and the DSC3k chain kernel, dsc3k_chain.hip)
+// LDS carve-up of one lean tile
 template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool PRE>
 struct LeanLds {
   static constexpr int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K, IWP = IW | 1, NQ = C / 4;
@@ -19,11 +18,9 @@ struct LeanLds {
   static constexpr int BYTES = P + (PRE ? 2 * PNP * 4 * 16 : 16);
 };
 
-// One TH x TW output tile (linear tile index `tile`: image-major, then tile row, tile column).  HO: the
-// activations are read and written with the in-launch hand-off accesses (sc1 buffer loads / stores,
-// conv_common.hpp) because another workgroup of the same launch produced or consumes them; the arithmetic is
-// the same either way.  smem: LeanLds::BYTES of LDS, 16-byte aligned.
-template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool TAIL, bool PRE, bool HO>
+// One TH x TW output tile (linear tile index `tile`: image-major, then tile row, tile column).
+// smem: LeanLds::BYTES of LDS, 16-byte aligned.
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool TAIL, bool PRE>
 __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const float* __restrict__ dww,
                                           const float* __restrict__ dwb, int dw_act, int tile, int tiles_x,
                                           int tiles_y, unsigned char* smem) {
@@ -67,19 +64,10 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
   h8* s_b = reinterpret_cast<h8*>(smem + L::B);      // pointwise B tile, [k-step][pixel][slot]
   h8* s_g = reinterpret_cast<h8*>(s_x);              // TG: trailing GEMM B tile (after the depthwise phase)
   h8* s_p = reinterpret_cast<h8*>(smem + L::P);      // PRE: the leading 1x1's B tile (g0x halo)
-  // activation accessors: plain, or the in-launch hand-off form (byte offsets from each view's base)
-  auto ld16 = [&](const T* base, int64_t off, bool ok) -> h8 {
-    if constexpr (HO) return ho_ld16(ho_rsrc(base), ok ? (unsigned)(off * 2) : HO_OOB);
-    else return vload_sel(base + off, base, ok);
-  };
-  auto ld8 = [&](const T* base, int64_t off) -> h4 {
-    if constexpr (HO) return ho_ld8(ho_rsrc(base), (unsigned)(off * 2));
-    else return *reinterpret_cast<const h4*>(base + off);
-  };
-  auto st8 = [&](T* base, int64_t off, const float* v) {
-    if constexpr (HO) ho_st8(ho_rsrc(base), (unsigned)(off * 2), to_h4_rne(v));
-    else store_f<4>(base + off, v);
-  };
+  // activation accessors (element offsets from each view's base)
+  auto ld16 = [&](const T* base, int64_t off, bool ok) -> h8 { return vload_sel(base + off, base, ok); };
+  auto ld8 = [&](const T* base, int64_t off) -> h4 { return *reinterpret_cast<const h4*>(base + off); };
+  auto st8 = [&](T* base, int64_t off, const float* v) { store_f<4>(base + off, v); };
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -226,10 +214,7 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
 #pragma unroll
         for (int q = 0; q < 4; ++q) v[q] = apply_act<T>(pa[q] + b0v[0][q], p.g0act);
         const h4 o = to_h4_rne(v);
-        if (outpx) {
-          if constexpr (HO) ho_st8(ho_rsrc(p.g0y), (unsigned)((((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.g0ycs + c) * 2), o);
-          else *reinterpret_cast<h4*>(p.g0y + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.g0ycs + c) = o;
-        }
+        if (outpx) *reinterpret_cast<h4*>(p.g0y + ((int64_t)(tl.b * p.H + iy) * p.W + ix) * p.g0ycs + c) = o;
         if (live) s_x[(hy * IWP + hx) * NQ + (c - C) / 4] = inimg ? o : h4{0, 0, 0, 0};
       }
       __syncthreads();
@@ -351,7 +336,6 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
         }
       }
     }
-    static_assert(!(HO && TAIL), "the class-conv tail has no hand-off form");
     if constexpr (TAIL && NCG == 1 && TN == 4 && !TG) {  // Detect class conv over the 64 output channels (CO == 64)
       conv_tail_1x1_vals<T, TN, TM>(p, ys, pp, pv, co, g);
     }

@@ -72,7 +72,10 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
 
   constexpr int TAPV = K * K * NQ;  // fp32 tap quads per chunk (392 for k7 f16: > one per thread)
   constexpr int TIT = (TAPV + 255) / 256;
+  // raw loads now, zero selects / tap rounding at the LDS store: the next chunk's loads stay in flight through
+  // this chunk's depthwise and pointwise phases (a select or conversion next to its load waits for it there)
   vec xr[HIT];
+  bool xok[HIT];
   f32x4 wr[TIT];
   auto load_chunk = [&](int c0) {
 #pragma unroll
@@ -81,16 +84,14 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
       const int cv = i & 3, px = i >> 2;
       const int hy = px / IW, hx = px - hy * IW;
       const int iy = iy0 + hy, ix = ix0 + hx;
-      const bool ok = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-      xr[it] = vload_sel(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + c0 + cv * VEC, p.x, ok);
+      xok[it] = iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      xr[it] = vload_clamped(p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + c0 + cv * VEC, p.x, xok[it]);
     }
 #pragma unroll
-    for (int it = 0; it < TIT; ++it) {  // taps rounded to the activation dtype (the reference's .half() weights)
+    for (int it = 0; it < TIT; ++it) {
       const int i = min(tid + it * 256, TAPV - 1);
       const int tap = i / NQ, q = i % NQ;
-      const f32x4 w = *reinterpret_cast<const f32x4*>(dww + tap * p.Cin + c0 + q * 4);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) wr[it][e] = float(T(w[e]));
+      wr[it] = *reinterpret_cast<const f32x4*>(dww + tap * p.Cin + c0 + q * 4);
     }
   };
   auto store_chunk = [&](int buf) {
@@ -101,14 +102,16 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
         const int cv = i & 3, px = i >> 2;
         const int hy = px / IW, hx = px - hy * IW;
         f32x4* d = &s_x[buf][(hy * IWP + hx) * NQ + cv * QV];
+        const vec xv = vsel(xr[it], xok[it]);
 #pragma unroll
         for (int u = 0; u < QV; ++u)
-          d[u] = f32x4{float(xr[it][4 * u]), float(xr[it][4 * u + 1]), float(xr[it][4 * u + 2]), float(xr[it][4 * u + 3])};
+          d[u] = f32x4{float(xv[4 * u]), float(xv[4 * u + 1]), float(xv[4 * u + 2]), float(xv[4 * u + 3])};
       }
     }
 #pragma unroll
-    for (int it = 0; it < TIT; ++it)
-      if (tid + it * 256 < TAPV) s_w[buf][tid + it * 256] = wr[it];
+    for (int it = 0; it < TIT; ++it)  // taps rounded to the activation dtype (the reference's .half() weights)
+      if (tid + it * 256 < TAPV)
+        s_w[buf][tid + it * 256] = f32x4{float(T(wr[it][0])), float(T(wr[it][1])), float(T(wr[it][2])), float(T(wr[it][3]))};
   };
 
   f32x4 acc[NTN][TMW];
@@ -124,13 +127,15 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
   for (int ch = 0; ch < nchunks; ++ch) {
     const int buf = DBUF ? (ch & 1) : 0;
     const int c0 = ch * CC;
-    if (ch + 1 < nchunks) load_chunk(c0 + CC);
+    // this chunk's pointwise A fragments first (loads complete in order: waiting for them later does not wait
+    // for the next chunk's), zero rows past Cout selected at the MFMAs
     vec af[NTN];
 #pragma unroll
     for (int i = 0; i < NTN; ++i) {
       const int co = co0 + i * 16 + r16;
-      af[i] = vload_sel(p.w + (int64_t)co * p.KPAD + c0 + g * VEC, p.w, co < p.Cout);
+      af[i] = vload_clamped(p.w + (int64_t)co * p.KPAD + c0 + g * VEC, p.w, co < p.Cout);
     }
+    if (ch + 1 < nchunks) load_chunk(c0 + CC);
     // ---- depthwise phase
     for (int task = tid; task < NTASK; task += 256) {
       const int q = task % NQ;
@@ -177,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
       if (t < NT) {
         const vec bf = s_b[bswz<0>(t * 16 + r16, g)];
 #pragma unroll
-        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_chunk<T>(af[i], bf, acc[i][j]);
+        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_chunk<T>(vsel(af[i], co0 + i * 16 + r16 < p.Cout), bf, acc[i][j]);
       }
     }
     if constexpr (DBUF) {
@@ -303,7 +308,7 @@ static int run_ds(const ydbl_dsconv_desc* d, hipStream_t s) {
   return fail(YDBL_EINVAL, "dsconv: supported (k, stride, dil): (3,1,1) (3,2,1) (5,1,1) (7,1,1)");
 }
 
-// The descriptor rules of ydbl_dsconv_nhwc (include/ydbl.h); also applied to every stage of ydbl_dsc3k_chain.
+// The descriptor rules of ydbl_dsconv_nhwc (include/ydbl.h).
 int ds_check(const ydbl_dsconv_desc* d) {
   if (!d) return fail(YDBL_EINVAL, "dsconv: null descriptor");
   if (check_view(&d->x, "dsconv.x", true) || check_view(&d->y, "dsconv.y", false)) return YDBL_EINVAL;

@@ -50,10 +50,6 @@ class DsConvDesc(C.Structure):
                 ("g0_x", View), ("g0_y", View), ("g0_act", C.c_int32)]
 
 
-class Dsc3kChainDesc(C.Structure):
-    _fields_ = [("st", DsConvDesc * 4), ("ctrl", C.c_void_p)]
-
-
 class HgDesc(C.Structure):
     _fields_ = [("x", View), ("xp", View), ("y", View), ("num_edges", C.c_int32), ("num_heads", C.c_int32),
                 ("proto_base", C.c_void_p), ("ctx_w", C.c_void_p), ("ctx_b", C.c_void_p),
@@ -131,9 +127,6 @@ SIGNATURES = {
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_pair_nhwc": ([C.POINTER(DwConvDesc), C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dsconv_nhwc": ([C.POINTER(DsConvDesc), _P], C.c_int),
-    "ydbl_dsc3k_chain": ([C.POINTER(Dsc3kChainDesc), _P], C.c_int),
-    "ydbl_dsc3k_chain_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
-    "ydbl_dsc3k_chain_status": ([_P, _P], C.c_int),
     "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
     "ydbl_conv_stem": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _P, _P, C.c_int32, C.c_int32,
                         C.c_int32, _VP, _P], C.c_int),

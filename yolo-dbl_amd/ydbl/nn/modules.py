@@ -216,21 +216,6 @@ def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Te
     return y
 
 
-def chain_steps(plan: Plan, n0: int) -> None:
-    """Replace the four ydbl_dsconv_nhwc launches plan.steps[n0:] of a fused DSC3k (stage order: k3 + leading 1x1,
-    k7 + residual, k3, k7 + residual + trailing cv3) by one ydbl_dsc3k_chain launch over the same descriptors
-    (bit-identical; the C-ABI checks the stages' data flow)."""
-    steps = plan.steps[n0:]
-    assert len(steps) == 4 and all(st.fn.__name__ == "ydbl_dsconv_nhwc" for st in steps), [s.what for s in steps]
-    x = steps[0].args[0].x
-    ctrl = plan.scratch(int(_lib.lib.ydbl_dsc3k_chain_workspace(x.n, x.h, x.w)), zero=True)
-    d = _lib.Dsc3kChainDesc((_lib.DsConvDesc * 4)(*[st.args[0] for st in steps]), ctrl.data_ptr())
-    keep = [k for st in steps for k in st.keep] + [d, ctrl]
-    del plan.steps[n0:]
-    plan.launch("ydbl_dsc3k_chain", d, what="DSC3k.chain", keep=keep)
-    plan.chain_ctrl.append(ctrl)
-
-
 def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = None, what="DWConv+Conv1x1",
                tail_conv: nn.Conv2d | None = None, tail_out: TV | None = None):
     """nn.Sequential(DWConv(c, c, k), Conv(c, c2, 1)) of the Detect head (head.py:93-101): one fused launch
@@ -564,14 +549,10 @@ class C3(nn.Module):
                     emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
                 mods = list(self.m)
                 t = buf.cslice(2 * c_, c_)
-                n0 = len(plan.steps)
                 for i, m in enumerate(mods[:-1]):
                     t = m.emit(plan, t, pre=pre if i == 0 else None)
-                y = mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
-                                  pre=pre if len(mods) == 1 else None)
-                if self._chain_ok(plan, x) and (pre is not None or c_ == 128):
-                    chain_steps(plan, n0)
-                return y
+                return mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
+                                     pre=pre if len(mods) == 1 else None)
             emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
             emit_seq(plan, self.m, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
             return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
@@ -581,16 +562,6 @@ class C3(nn.Module):
         self.cv2.emit(plan, x, buf.cslice(c_, c_))
         return self.cv3.emit(plan, buf, out)
 
-
-    def _chain_ok(self, plan, x) -> bool:
-        """The four DSConv launches of a fused DSC3k (two k3 / k7 DSBottlenecks + trailing cv3, and the leading 1x1
-        at c_ 64) as one ydbl_dsc3k_chain launch (csrc/dsc3k_chain.hip); YDBL_DSC3K_CHAIN=0 keeps the four."""
-        def ds_ok(ds, k):
-            return ds.dw.kernel_size == (k, k) and ds.dw.stride == (1, 1) and ds.dw.dilation == (1, 1)
-
-        return (os.environ.get("YDBL_DSC3K_CHAIN") != "0" and plan.dtype == torch.float16
-                and self.cv1.conv.out_channels in (64, 128) and len(self.m) == 2
-                and all(isinstance(m, DSBottleneck) and m.add and ds_ok(m.cv1, 3) and ds_ok(m.cv2, 7) for m in self.m))
 
     def _cv1_fusable(self, plan, x) -> bool:
         """cv2 | cv1 (merged 1x1, x.c -> 2 c_) can lead the first DSBottleneck's k3 DSConv in one launch

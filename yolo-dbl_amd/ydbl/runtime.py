@@ -86,7 +86,6 @@ class Plan:
         self.bytes_allocated = 0
         self._writers: dict = {}  # view key -> (step index, desc) of the conv / DySample launch that wrote it
         self.fp8_candidates: list = []  # (ConvDesc, input view, fp32 [Cout][KPAD] weights) of fp8-able convs
-        self.chain_ctrl: list = []  # control blocks of the in-launch pipelined chains (ydbl_dsc3k_chain)
 
     # ---------------------------------------------------------------- memory
     def alloc(self, n: int, h: int, w: int, c: int, dtype: torch.dtype | None = None, cs: int | None = None) -> TV:
@@ -148,11 +147,6 @@ class Plan:
         d.y2, d.r2, d.a2, d.b2 = y2.struct(), r2.struct(), float(a2), float(b2)
         self.steps[writer[0]].keep.append((y2, r2))
         return y2
-
-    def chain_errors(self) -> int:
-        """Control blocks whose stage waits timed out since allocation (ydbl_dsc3k_chain_status; syncs)."""
-        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
-        return sum(1 for c in self.chain_ctrl if lib.ydbl_dsc3k_chain_status(c.data_ptr(), s) != 0)
 
     def run(self, stream: int | None = None):
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream if stream is None else stream)
