@@ -1,5 +1,9 @@
-"""DBL-s 640 fp8 (BASELINE config 5): mAP50 drop vs the CPU oracle under the config-5 protocol
-(tests/test_gpu_model.py::test_map50_config5_dbl_s_640) for a sweep of e4m3 MAC fractions."""
+"""DBL-s 640 fp8 (BASELINE config 5): mAP50 drop vs the CPU oracle under the config-5 protocol of
+tests/test_gpu_model.py::test_map50_config5_dbl_s_640 (all 16 blob images, pseudo-GT = the oracle's fp32 detections
+at conf 0.0171, val at conf 0.001) for a sweep of e4m3 MAC fractions, with and without ydbl.quant's bias correction.
+
+    python scripts/fp8_sweep.py [fraction ...]      (default: 0.1 0.25 0.5 1.0)
+"""
 import sys
 from pathlib import Path
 
@@ -9,10 +13,12 @@ import torch  # noqa: E402
 
 import test_gpu_model as T  # noqa: E402
 from oracle.ops import clip_boxes, non_max_suppression  # noqa: E402
+from ydbl import quant  # noqa: E402
 from ydbl.utils.synthetic import blob_images  # noqa: E402
 
+fracs = [float(a) for a in sys.argv[1:]] or [0.1, 0.25, 0.5, 1.0]
 p, o = T._models("yolov13s_DBL.yaml", 3, ROOT / "tests" / "golden")
-x = blob_images(16, 640, seed=1234)[[3, 13, 14, 15]]
+x = blob_images(16, 640, seed=1234)
 with torch.no_grad():
     y, _ = o(x)
 gt_conf = 0.0171
@@ -22,7 +28,19 @@ for g in non_max_suppression(y, gt_conf, 0.7):
     labels.append(torch.cat([g[:, 5:6], g[:, :4]], 1))
 batch = {"img": x, "cls": torch.cat([lb[:, 0] for lb in labels]), "bboxes": torch.cat([lb[:, 1:] for lb in labels]),
          "batch_idx": torch.cat([torch.full((len(lb),), i) for i, lb in enumerate(labels)])}
-m_cpu = T._cpu_map50(o, x, labels, conf=gt_conf / 2)
-for frac in (False, 0.25, 0.5, 0.75, 0.9, True):
-    m = p.val(data=[batch], half=True, fp8=frac, conf=gt_conf / 2).box.map50
-    print(f"fp8 fraction {frac}: mAP50 gpu {m:.4f} cpu {m_cpu:.4f} drop {m_cpu - m:+.4f}", flush=True)
+m_cpu = T._cpu_map50(o, x, labels, conf=0.001)
+m16 = p.val(data=[batch], half=True, fp8=False, conf=0.001).box.map50
+print(f"fp16: mAP50 gpu {m16:.4f} cpu {m_cpu:.4f} drop {m_cpu - m16:+.4f}", flush=True)
+orig = quant.enable_fp8
+for bc in (True, False):
+    def patched(*a, _bc=bc, **k):
+        k["bias_correct"] = _bc
+        return orig(*a, **k)
+    quant.enable_fp8 = patched
+    for frac in fracs:
+        p._sessions.clear()
+        m = p.val(data=[batch], half=True, fp8=True if frac >= 1 else frac, conf=0.001).box.map50
+        got = [s.fp8_mac_fraction for s in p._sessions.values() if s.fp8][-1]
+        print(f"fp8 fraction {frac} (achieved {got:.3f}) bias correction {'on ' if bc else 'off'}: mAP50 gpu {m:.4f} "
+              f"cpu {m_cpu:.4f} drop {m_cpu - m:+.4f}", flush=True)
+quant.enable_fp8 = orig

@@ -1,6 +1,6 @@
 """ydbl_nms alone on the bench's own candidates (DBL-n 640 bs32 fp16, synthetic blob images, trained-like
 weights): per-image candidate counts and class mix, HIP-event time per launch for the class-split and
-the one-workgroup-per-image forms, and (with the stamps build, scripts/build_nms_stamps.sh, YDBL_LIB
+the one-workgroup-per-image forms, and (with the stamps build, scripts/build_stamps.sh detect, YDBL_LIB
 pointing at it) the slowest workgroup's phase split.
 
     python scripts/nms_real.py [--stamps]

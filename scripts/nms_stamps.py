@@ -1,4 +1,4 @@
-"""NMS phase timing from the diagnostic build (scripts/build_nms_stamps.sh): per-workgroup
+"""NMS phase timing from the diagnostic build (scripts/build_stamps.sh detect): per-workgroup
 s_memrealtime stamps (100 MHz) at start / sorted / staged / swept, plus rounds and list length."""
 import ctypes as C
 import os

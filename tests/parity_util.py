@@ -231,7 +231,7 @@ def fp8_emulated_leg(o, x, plan):
     half=True path, evaluated by torch-CPU) with every convolution / linear layer that the GPU `plan` switched to
     e4m3 operands (ydbl.quant.enable_fp8: plan.fp8_switched) replaced by its e4m3 emulation at the GPU's
     calibrated scales: input x -> e4m3(x * qs) / qs, weights per output row -> e4m3(w * sw) / sw with
-    sw = 448 / max|w_row|, then the fp32 conv + bias.  The plan's candidates are matched to the oracle's modules
+    sw = 448 / max|w_row|, then the fp32 conv + the bias the GPU plan uses (bias correction included).  The plan's candidates are matched to the oracle's modules
     by their (scale-normalised) weight rows, so merged launches (C3's cv2 + cv1) and folded constants
     (DySample's 0.25) map back to the reference's own layers.  Returns (decoded predictions [B, 4+nc, A] fp32,
     number of oracle layers emulated)."""
@@ -242,13 +242,15 @@ def fp8_emulated_leg(o, x, plan):
 
     from ydbl.quant import E4M3_MAX, e4m3_round
 
-    rows, owner = [], []  # normalised leading 16 values of every switched candidate row, and (qs, cin_pad)
-    for ci in plan.fp8_switched:
+    rows, owner, dl = [], [], []  # normalised leading 16 values of every switched candidate row, (qs, cin_pad),
+    for ci in plan.fp8_switched:  # and the row's bias correction (ydbl.quant.bias_delta; 0 without)
         d, xv, w32 = plan.fp8_candidates[ci]
         w = w32[:, : d.kh * d.kw * xv.c].double()
         w = w / w.abs().amax(1, keepdim=True).clamp_min(1e-30)
         rows.append(w[:, :16])
         owner += [(float(d.qscale), xv.c)] * w.shape[0]
+        dl.append(getattr(plan, "fp8_bias_delta", {}).get(ci, torch.zeros(w.shape[0])).float())
+    dl = torch.cat(dl) if dl else None
     if not rows:
         raise ValueError("the plan has no fp8-switched convolutions")
     rows = torch.cat(rows)
@@ -273,7 +275,7 @@ def fp8_emulated_leg(o, x, plan):
             dev = (rows[:, : len(r)] - r).abs().amax(1)
             j = int(dev.argmin())
             if dev[j] < 1e-5 and owner[j][1] == cin_pad:
-                hit = owner[j]
+                hit = owner[j] + (dl[j: j + co],)
                 break
         if hit is None:
             continue
@@ -282,7 +284,8 @@ def fp8_emulated_leg(o, x, plan):
         sw = E4M3_MAX / w32.reshape(co, -1).abs().amax(1).clamp_min(1e-12)
         shape = (-1,) + (1,) * (w32.dim() - 1)
         wq = e4m3_round(w32 * sw.view(shape)) / sw.view(shape)
-        b32 = ref_mod.bias.detach().float() if ref_mod.bias is not None else None
+        b32 = ref_mod.bias.detach().float() if ref_mod.bias is not None else torch.zeros(co)
+        b32 = b32 - hit[2]  # the GPU's bias correction of this layer
 
         def fwd(self, inp, wq=wq, b32=b32, qs=qs, conv=isinstance(ref_mod, nn.Conv2d)):
             xq = e4m3_round(inp.float() * qs) / qs

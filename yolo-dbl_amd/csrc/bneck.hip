@@ -121,6 +121,20 @@ __device__ __forceinline__ int kbase(int g) {
   return CH >= 4 ? g * PL * 16 : 0;
 }
 
+// Diagnostic build only (-DYDBL_BNECK_STAMPS, scripts/bneck_stamps.py): per-workgroup s_memrealtime stamps (100 MHz)
+// when wave 0 starts, has staged the window, has finished cv1, has stored cv2; plus the hardware ids.
+#ifdef YDBL_BNECK_STAMPS
+__device__ unsigned long long g_bn_stamps[8 * 16384];
+#define BN_STAMP(k)                                                                                         \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_bn_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define BN_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 template <int C, int CMID, int TH, bool ADD, bool PW = false, int CIN = C>
 __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, DView<_Float16> y,
                                                        const unsigned char* __restrict__ params, int tiles_x,
@@ -141,6 +155,16 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
+  BN_STAMP(0);
+#ifdef YDBL_BNECK_STAMPS
+  if (tid == 0 && blockIdx.x < 16384) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_bn_stamps[blockIdx.x * 8 + 4] = hw;
+    g_bn_stamps[blockIdx.x * 8 + 5] = xcc;
+  }
+#endif
   const int t = (ntiles & 7) ? (int)blockIdx.x : xcd_remap(blockIdx.x, ntiles);
   const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y;
   const int img = t / (tiles_x * tiles_y);
@@ -189,6 +213,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
   const unsigned char* in_b = s_in + kbase<CH, PIN>(g);
   const bool interior = oy0 >= 1 && ox0 >= 1 && oy0 + TH + 1 <= y.h && ox0 + Cfg::TW + 1 <= y.w;
   __syncthreads();
+  BN_STAMP(1);
 
   // ---- 2. cv1 over the virtual grid: MR rows x IP columns, mid pixel v reads input record v + tap.
   // Two 16-pixel groups per iteration (independent accumulators: the LDS reads of one overlap the
@@ -233,6 +258,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     for (int m = 0; m < KS2; ++m) a2[m] = w2f[(t2 * KS2 + m) * 64 + lane];
   }
   __syncthreads();
+  BN_STAMP(2);
 
   // ---- 3. cv2: output rows j, j + WPT2 of the tile, 16 columns = the 16 lanes
   auto epi2 = [&](const f32x4& acc, int j) {
@@ -273,6 +299,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     epi2(acc0, j);
     if (two) epi2(acc1, j1);
   }
+  BN_STAMP(3);
 
   if constexpr (PW) {
     // ---- 4. trailing 1x1 conv C -> C + bias (Detect box branch cv2[i][2], head.py:86-90) over the
@@ -320,6 +347,16 @@ static int64_t pair_bytes(int c, int cm) {
   if (c == 64 && cm == 64) return BneckCfg<64, 64, 16>::BYTES;
   return -1;
 }
+
+#ifdef YDBL_BNECK_STAMPS
+extern "C" int ydbl_bneck_debug_stamps(unsigned long long* out, int32_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bn_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" int ydbl_bneck_debug_reset() {
+  static unsigned long long zeros[8 * 16384];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_bn_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int64_t ydbl_bottleneck_params_size(int32_t c) { return pair_bytes(c, c / 2); }
 extern "C" int64_t ydbl_conv3x3_pair_params_size(int32_t c, int32_t c_mid) { return pair_bytes(c, c_mid); }

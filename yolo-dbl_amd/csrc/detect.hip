@@ -287,7 +287,7 @@ __device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4
   return (double)ovr > thr;
 }
 
-// Diagnostic build only (-DYDBL_NMS_STAMPS, scripts/nms_stamps.sh): per-workgroup phase timestamps.
+// Diagnostic build only (-DYDBL_NMS_STAMPS, scripts/build_stamps.sh detect, scripts/nms_stamps.py): per-workgroup phase timestamps.
 #ifdef YDBL_NMS_STAMPS
 __device__ unsigned long long g_nms_stamps[16 * 4096];
 #define NMS_STAMP(k, v) \

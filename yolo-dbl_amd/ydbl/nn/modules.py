@@ -93,6 +93,7 @@ def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None
     plan.launch("ydbl_conv2d_nhwc", d, what=what, keep=[wd, bd, d])
     plan.note_writer(y, d)
     if plan.dtype == torch.float16 and x.c >= 64 and not what.startswith("Detect."):
+        d._b32 = b.detach().float().cpu() if b is not None else None  # (ydbl.quant's bias correction)
         plan.fp8_candidates.append((d, x, wk32))  # see ydbl.quant: e4m3 operands after calibration
 
 

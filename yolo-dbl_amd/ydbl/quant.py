@@ -11,6 +11,12 @@ Layers kept in fp16: convs with fewer than 64 input channels (stem and the thin 
 backbone convs), depthwise / DSConv / attention / hypergraph kernels, and the Detect head's
 final box / class 1x1 convs.  Activations are stored in fp16 between layers.
 
+Bias correction (on by default): e4m3 rounding of the weights and of the activations shifts each output channel's
+mean; with mu_c / muq_c the per-channel means of the layer's input before / after e4m3 rounding over the calibration
+batch, the fp8 layer gets bias b - (sum_k wq[co][k] muq_c(k) - sum_k w[co][k] mu_c(k)) (k over taps x channels,
+c(k) its input channel), so its pre-activation mean matches the fp16 layer's (the empirical bias correction of
+data-free / post-training quantization; zero padding at the borders is ignored).
+
 Mixed selection (fraction < 1): every candidate is first switched to e4m3 ALONE and the perturbation
 of the Detect head outputs (all levels, mean |delta| over the fp16 run) recorded; the candidates are
 then switched in increasing-sensitivity order until `fraction` of the candidates' MACs run in e4m3 --
@@ -34,11 +40,29 @@ def quantize_weights_e4m3(w: torch.Tensor):
 
 
 def _switch(d, state):
-    """Set a conv descriptor's operand mode: state None -> fp16, else (w e4m3 ptr, dq ptr, qs)."""
+    """Set a conv descriptor's operand mode: state None -> fp16, else (w e4m3 ptr, dq ptr, qs, bias ptr)."""
     if state is None:
-        d.w, d.dq, d.qscale = d._w16, None, 1.0
+        d.w, d.dq, d.qscale, d.bias = d._w16, None, 1.0, d._bias16
     else:
-        d.w, d.dq, d.qscale = state
+        d.w, d.dq, d.qscale, d.bias = state
+
+
+def bias_delta(xs, qs, w32, wq, sw, kk):
+    """Per-output-channel shift of an e4m3 conv's pre-activation mean (module docstring): xs = the layer's input
+    activations over the calibration batch ([..., C] tensors, one per sub-batch plan), w32 = fp32 [Cout][KPAD]
+    tap-major weights, (wq, sw) their e4m3 bytes and row scales, kk = kh * kw.  Returns fp32 [Cout] (CPU)."""
+    tot = mu = muq = 0
+    for x in xs:
+        xf = x.float().reshape(-1, x.shape[-1])
+        mu = mu + xf.sum(0)
+        muq = muq + (e4m3_round(xf * qs) / qs).sum(0)
+        tot += xf.shape[0]
+    mu, muq = (mu / tot).double().cpu(), (muq / tot).double().cpu()
+    c = mu.numel()
+    cout = w32.shape[0]
+    w = w32[:, : kk * c].double().reshape(cout, kk, c)
+    wdq = (wq.view(torch.float8_e4m3fn).float().double() / sw.double()[:, None])[:, : kk * c].reshape(cout, kk, c)
+    return ((wdq * muq).sum((1, 2)) - (w * mu).sum((1, 2))).float()
 
 
 def candidate_macs(cand) -> int:
@@ -62,7 +86,7 @@ def select_by_mac_budget(sens, macs, fraction):
     return sorted(chosen), (used / sum(macs) if macs else 0.0)
 
 
-def enable_fp8(plans, run_calibration, select=None, fraction=1.0, head=None) -> int:
+def enable_fp8(plans, run_calibration, select=None, fraction=1.0, head=None, bias_correct=True) -> int:
     """Calibrate activation scales with one fp16 pass and switch fp8 candidate convs to e4m3 operands.
 
     `plans`: one Plan, or the per-sub-batch plans of a split session (built from the same model, so their
@@ -82,16 +106,26 @@ def enable_fp8(plans, run_calibration, select=None, fraction=1.0, head=None) -> 
         return 0
     amax = torch.stack([torch.stack([p.fp8_candidates[i][1].torch().abs().amax().float() for i in idx]).cpu()
                         for p in plans]).amax(0)
-    states = [[] for _ in plans]  # per plan, per selected candidate: (w e4m3 ptr, dq ptr, qs)
+    states = [[] for _ in plans]  # per plan, per selected candidate: (w e4m3 ptr, dq ptr, qs, bias ptr)
+    for p in plans:
+        p.fp8_bias_delta = {}
     for k, (i, ax) in enumerate(zip(idx, amax.tolist())):
         qs = E4M3_MAX / ax if ax > 0 else 1.0
-        wq, sw = quantize_weights_e4m3(plans[0].fp8_candidates[i][2])
+        d0, _, w32 = plans[0].fp8_candidates[i]
+        wq, sw = quantize_weights_e4m3(w32)
         dqv = (1.0 / (sw * qs)).float()
+        b8 = d0._b32.clone() if getattr(d0, "_b32", None) is not None else torch.zeros(w32.shape[0])
+        if bias_correct:
+            delta = bias_delta([p.fp8_candidates[i][1].torch() for p in plans], qs, w32, wq, sw, d0.kh * d0.kw)
+            b8 = b8 - delta
+            for p in plans:
+                p.fp8_bias_delta[i] = delta
         for pi, p in enumerate(plans):
             d = p.fp8_candidates[i][0]
             if not hasattr(d, "_w16"):
-                d._w16 = d.w
-            states[pi].append((p.const(wq.contiguous()).data_ptr(), p.const(dqv).data_ptr(), float(qs)))
+                d._w16, d._bias16 = d.w, d.bias
+            states[pi].append((p.const(wq.contiguous()).data_ptr(), p.const(dqv).data_ptr(), float(qs),
+                               p.const(b8.float()).data_ptr()))
     chosen = list(range(len(idx)))
 
     def switch(k, on):
