@@ -650,7 +650,7 @@ def test_bottleneck_rejects_bad_shapes():
     assert _lib.lib.ydbl_bottleneck_nhwc(ctypes.byref(d), None) != 0
 
 
-def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False):
+def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False, whats=()):
     """Run oracle module (CPU fp32) and product module (GPU) on the same inputs/weights."""
     p_mod.load_state_dict(o_mod.state_dict())
     with torch.no_grad():
@@ -658,6 +658,8 @@ def _module_parity(o_mod, p_mod, xs, dtype, tol, multi=False):
     plan = _plan(dtype)
     views = [_tv_from_nchw(plan, x) for x in xs]
     out = p_mod.emit(plan, views if multi else views[0])
+    for w in whats:  # launches the plan builder must have emitted (fusion rules)
+        assert any(st.what == w for st in plan.steps), (w, [st.what for st in plan.steps])
     _run(plan)
     got = out.nchw().float().cpu()
     torch.testing.assert_close(got, ref, **tol)
@@ -752,7 +754,8 @@ def test_hyperace(dtype):
     o = om.HyperACE(*args).eval()
     xs = [torch.randn(2, 64, 16, 16), torch.randn(2, 64, 8, 8), torch.randn(2, 128, 4, 4)]
     tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=3e-2, atol=3e-2)
-    _module_parity(o, M.HyperACE(*args), xs, dtype, tol, multi=True)
+    # both C3AH branches' input 1x1s as one launch (HyperACE._emit_branches)
+    _module_parity(o, M.HyperACE(*args), xs, dtype, tol, multi=True, whats=("C3AHx2.cv1|cv2",))
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])

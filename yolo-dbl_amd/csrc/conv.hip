@@ -612,7 +612,7 @@ static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
 }
 
 template <typename T>
-static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
+static ConvArgs<T> conv_args(const ydbl_conv_desc* d) {
   ConvArgs<T> a{};
   a.x = reinterpret_cast<const T*>(d->x.ptr);
   a.xcs = d->x.cs; a.N = d->x.n; a.H = d->x.h; a.W = d->x.w; a.Cin = d->x.c;
@@ -628,6 +628,14 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   a.r2 = reinterpret_cast<const T*>(d->r2.ptr); a.r2cs = d->r2.cs;
   a.a2 = d->a2; a.b2 = d->b2;
   a.dq = d->dq; a.qs = d->qscale;
+  return a;
+}
+
+ConvArgs<_Float16> conv_args_f16(const ydbl_conv_desc* d) { return conv_args<_Float16>(d); }
+
+template <typename T>
+static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
+  const ConvArgs<T> a = conv_args<T>(d);
   const bool pw = d->kh == 1 && d->kw == 1 && d->stride == 1 && d->pad == 0 && d->x.h == d->y.h && d->x.w == d->y.w;
   if constexpr (sizeof(T) == 2) {
     if (d->dq) {
@@ -639,11 +647,8 @@ static int run_conv(const ydbl_conv_desc* d, hipStream_t s) {
   return check_launch("ydbl_conv2d_nhwc");
 }
 
-}  // namespace ydbl
-
-using namespace ydbl;
-
-extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
+// The descriptor rules of ydbl_conv2d_nhwc (include/ydbl.h).
+int conv_check(const ydbl_conv_desc* d) {
   if (!d) return fail(YDBL_EINVAL, "conv: null descriptor");
   if (check_view(&d->x, "conv.x", true) || check_view(&d->y, "conv.y", false)) return YDBL_EINVAL;
   if (d->x.dtype != d->y.dtype) return fail(YDBL_EINVAL, "conv: x/y dtype mismatch");
@@ -672,6 +677,15 @@ extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
     };
     if (!same(d->y2) || !same(d->r2)) return fail(YDBL_EINVAL, "conv: y2/r2 must match y (shape, dtype, cs % 4)");
   }
+  return YDBL_OK;
+}
+
+}  // namespace ydbl
+
+using namespace ydbl;
+
+extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
+  if (const int rc = conv_check(d)) return rc;
   const hipStream_t s = as_stream(stream);
   return d->x.dtype == YDBL_F16 ? run_conv<_Float16>(d, s) : run_conv<float>(d, s);
 }

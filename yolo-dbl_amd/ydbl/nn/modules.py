@@ -835,12 +835,37 @@ class HyperACE(nn.Module):
         cat = plan.alloc(x.n, x.h, x.w, (4 + n) * c)
         self.cv1.emit(plan, x, cat.cslice(0, 3 * c))  # y0 | y1 | y2
         y1 = cat.cslice(c, c)
-        self.branch2.emit(plan, y1, cat.cslice((3 + n) * c, c))
-        self.branch1.emit(plan, y1, cat.cslice(c, c))  # reads y1 before its last conv overwrites it
+        if self._branches_mergeable():
+            self._emit_branches(plan, y1, cat.cslice(c, c), cat.cslice((3 + n) * c, c))
+        else:
+            self.branch2.emit(plan, y1, cat.cslice((3 + n) * c, c))
+            self.branch1.emit(plan, y1, cat.cslice(c, c))  # reads y1 before its last conv overwrites it
         prev = cat.cslice(2 * c, c)
         for i, m in enumerate(self.m):
             prev = m.emit(plan, prev, cat.cslice((3 + i) * c, c))
         return self.cv2.emit(plan, cat, out)
+
+
+    def _branches_mergeable(self) -> bool:
+        b1, b2 = self.branch1, self.branch2
+        return (not os.environ.get("YDBL_NO_MERGE") and mergeable([b2.cv2, b2.cv1, b1.cv1, b1.cv2])
+                and b1.cv1.conv.out_channels == b2.cv1.conv.out_channels)
+
+    def _emit_branches(self, plan, y1, out1, out2):
+        """Both C3AH branches read y1 (block.py:1886-1895): their four input 1x1s (cv1, cv2 of each) run as ONE
+        launch into one buffer laid out [b2.m | b2.cv2 | b2.cv1 | b1.cv1 | b1.cv2 | b1.m], so each branch's
+        cv3 input is contiguous: b2's in the reference order cat(m, cv2), b1's as (cv2, m) with cv3's weight
+        columns swapped to match (the same sums, in another order of K)."""
+        b1, b2 = self.branch1, self.branch2
+        c_ = b1.cv1.conv.out_channels
+        bb = plan.alloc(y1.n, y1.h, y1.w, 6 * c_)
+        emit_merged(plan, [b2.cv2, b2.cv1, b1.cv1, b1.cv2], y1, bb.cslice(c_, 4 * c_), what="C3AHx2.cv1|cv2")
+        b2.m.emit(plan, bb.cslice(2 * c_, c_), bb.cslice(0, c_))
+        b2.cv3.emit(plan, bb.cslice(0, 2 * c_), out2)
+        b1.m.emit(plan, bb.cslice(3 * c_, c_), bb.cslice(5 * c_, c_))
+        w, b = b1.cv3.folded()
+        w = torch.cat([w[:, c_:], w[:, :c_]], 1)
+        emit_conv2d(plan, b1.cv3.conv, bb.cslice(4 * c_, 2 * c_), out1, w, b, _act_code(b1.cv3.act), what="Conv1x1")
 
 
 class DownsampleConv(nn.Module):
