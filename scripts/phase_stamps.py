@@ -1,8 +1,8 @@
-"""Bottleneck phase timing from the diagnostic build (scripts/build_stamps.sh bneck): per-workgroup s_memrealtime
-stamps (100 MHz) when wave 0 starts / has staged the input window / has finished cv1 / has stored cv2, and the
-hardware ids (XCD, SE, CU).  Prints phase medians and how many workgroups each CU held at once over the launch.
+"""Phase timing from the diagnostic builds (scripts/build_stamps.sh bneck|stem2): per-workgroup s_memrealtime
+stamps (100 MHz) when wave 0 starts / has staged the input window / has finished the first conv / has stored the
+second, and the hardware ids (XCD, SE, CU).  Prints phase medians and how many workgroups each CU held at once.
 
-    python scripts/bneck_stamps.py [c64@80 ...]   (kbench case substrings; default: the three DBL-n backbone shapes)
+    python scripts/bneck_stamps.py [--stem2] [c64@80 ...]   (kbench case substrings; default: the DBL-n backbone)
 """
 import ctypes as C
 import os
@@ -10,7 +10,8 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
-os.environ["YDBL_LIB"] = str(ROOT / "build_dbg" / "libydbl_bneck_stamps.so")
+KIND = "stem2" if "--stem2" in sys.argv else "bneck"
+os.environ["YDBL_LIB"] = str(ROOT / "build_dbg" / f"libydbl_{KIND}_stamps.so")
 sys.path.insert(0, str(ROOT / "yolo-dbl_amd"))
 sys.path.insert(0, str(ROOT / "scripts"))
 import numpy as np  # noqa: E402
@@ -19,7 +20,9 @@ import torch  # noqa: E402
 import kbench  # noqa: E402
 from ydbl import _lib  # noqa: E402
 
-sel = sys.argv[1:] or ["bneck c16@320", "bneck c32@160", "bneck c64@80", "box3 64@80"]
+sel = [a for a in sys.argv[1:] if a != "--stem2"] or (["stem2"] if KIND == "stem2" else
+                                                      ["bneck c16@320", "bneck c32@160", "bneck c64@80", "box3 64@80"])
+get, reset = getattr(_lib.lib, f"ydbl_{KIND}_debug_stamps"), getattr(_lib.lib, f"ydbl_{KIND}_debug_reset")
 for name, build in kbench.CASES:
     if not any(s in name for s in sel):
         continue
@@ -27,12 +30,12 @@ for name, build in kbench.CASES:
     for _ in range(2):
         plan.run()
     torch.cuda.synchronize()
-    assert _lib.lib.ydbl_bneck_debug_reset() == 0
+    assert reset() == 0
     plan.run()
     torch.cuda.synchronize()
     n = 16384
     buf = np.zeros(8 * n, dtype=np.uint64)
-    assert _lib.lib.ydbl_bneck_debug_stamps(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), len(buf)) == 0
+    assert get(buf.ctypes.data_as(C.POINTER(C.c_ulonglong)), len(buf)) == 0
     st = buf.reshape(-1, 8).astype(np.int64)
     st = st[st[:, 0] > 0]
     t0 = st[:, 0].min()

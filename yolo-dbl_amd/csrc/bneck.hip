@@ -121,7 +121,7 @@ __device__ __forceinline__ int kbase(int g) {
   return CH >= 4 ? g * PL * 16 : 0;
 }
 
-// Diagnostic build only (-DYDBL_BNECK_STAMPS, scripts/bneck_stamps.py): per-workgroup s_memrealtime stamps (100 MHz)
+// Diagnostic build only (-DYDBL_BNECK_STAMPS, scripts/phase_stamps.py): per-workgroup s_memrealtime stamps (100 MHz)
 // when wave 0 starts, has staged the window, has finished cv1, has stored cv2; plus the hardware ids.
 #ifdef YDBL_BNECK_STAMPS
 __device__ unsigned long long g_bn_stamps[8 * 16384];

@@ -83,6 +83,20 @@ void stem2_pack(const float* w0, const float* b0, const float* w1, const float* 
   for (int i = 0; i < Cfg::C1; ++i) fb1[i] = b1[i];
 }
 
+// Diagnostic build only (-DYDBL_STEM2_STAMPS, scripts/build_stamps.sh stem2): per-workgroup s_memrealtime stamps
+// (100 MHz) when wave 0 starts, has staged the window, has finished the first conv, has stored; + hardware ids.
+#ifdef YDBL_STEM2_STAMPS
+__device__ unsigned long long g_st_stamps[8 * 16384];
+#define ST_STAMP(k)                                                                                         \
+  do {                                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 16384) g_st_stamps[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define ST_STAMP(k) \
+  do {              \
+  } while (0)
+#endif
+
 // One workgroup per tile.  (Measured and not kept: a persistent walk over 2-8 tiles per CU with the next
 // tile's window prefetched during the current tile's convs -- 140-166 vs 136 us at bs32: the kernel is VALU-
 // issue-bound on the first conv's SiLU, not latency-bound.)
@@ -221,11 +235,22 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
 #pragma unroll
     for (int q = 0; q < 4; ++q) bias1[t][q] = b1[16 * t + 4 * g + q];
 
+  ST_STAMP(0);
+#ifdef YDBL_STEM2_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < 16384) {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    g_st_stamps[blockIdx.x * 8 + 4] = hw;
+    g_st_stamps[blockIdx.x * 8 + 5] = xcc;
+  }
+#endif
   const Tile tl = tile_of(blockIdx.x);
   load_window(tl);
   {
     store_window();
     __syncthreads();
+    ST_STAMP(1);
     // workgroups whose first-conv window lies inside the image skip the per-pixel padding test
     const bool interior = tl.Y0 >= 0 && tl.X0 >= 0 && tl.Y0 + Cfg::L0H <= H && tl.X0 + Cfg::L0W <= W;
 
@@ -268,6 +293,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
     if (interior) conv1(std::true_type{});
     else conv1(std::false_type{});
     __syncthreads();
+    ST_STAMP(2);
 
     // ---- 3. second conv: TH rows x TW cols, 16-pixel row segments
     constexpr int SEG = TW / 16;
@@ -295,11 +321,22 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
       }
     }
   }
+  ST_STAMP(3);
 }
 
 }  // namespace ydbl
 
 using namespace ydbl;
+
+#ifdef YDBL_STEM2_STAMPS
+extern "C" int ydbl_stem2_debug_stamps(unsigned long long* out, int32_t n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_st_stamps), (size_t)n * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" int ydbl_stem2_debug_reset() {
+  static unsigned long long zeros[8 * 16384];
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_st_stamps), zeros, sizeof(zeros)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 extern "C" int64_t ydbl_conv_stem2_params_size(int32_t c0) {
   if (c0 == 8) return Stem2Cfg<8, 32, 8>::BYTES;
