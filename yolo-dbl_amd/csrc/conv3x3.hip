@@ -27,7 +27,7 @@ __device__ __forceinline__ int hslot(int pix, int g) {
   return (pix / (16 * S)) * (64 * S) + g * (16 * S) + (pix % S) * 16 + ((pix / S) & 15);
 }
 
-template <typename T, int S, int TH, int NTN, bool Q8, int PF = 1>
+template <typename T, int S, int TH, int NTN, bool Q8>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int tiles_x, int tiles_y,
                                                               int co_splits) {
   constexpr int TW = 16;
@@ -86,26 +86,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     wok[it] = co < p.Cout;
     wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
-  // PF register slots of chunks in flight (chunk c in slot c % PF from its load, PF chunks before it is
-  // computed, until its LDS store): raw loads, zero selects at the LDS store (vload_clamped); past the last
-  // chunk a load is a masked no-op, so for PF > 1 the loads are unconditional and the waitcnt pass sees one order
-  vec xr[PF][XIT];
-  opv wr[PF][WIT];
-  bool cok[PF];
-  auto load_chunk = [&](int c0, vec (&xs)[XIT], opv (&ws)[WIT], bool& ok) {
-    ok = c0 < p.Cin;
+  // raw loads, zero selects at the LDS store (vload_clamped): the next chunk stays in flight during the MFMAs
+  vec xr[XIT];
+  opv wr[WIT];
+  bool cok = true;
+  auto load_chunk = [&](int c0) {
+    cok = c0 < p.Cin;
 #pragma unroll
-    for (int it = 0; it < XIT; ++it) xs[it] = vload_clamped(xsrc[it] + c0, p.x, xok[it] && ok);
+    for (int it = 0; it < XIT; ++it) xr[it] = vload_clamped(xsrc[it] + c0, p.x, xok[it] && cok);
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) ws[it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0, wok[it] && ok);
+    for (int it = 0; it < WIT; ++it) wr[it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0, wok[it] && cok);
   };
-  auto store_chunk = [&](const vec (&xs)[XIT], const opv (&ws)[WIT], bool ok) {
+  auto store_chunk = [&]() {
 #pragma unroll
     for (int it = 0; it < XIT; ++it)
-      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(vsel(xs[it], xok[it] && ok), p.qs);
+      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
 #pragma unroll
     for (int it = 0; it < WIT; ++it)
-      if (it * 256 + tid < WV) s_w[it * 256 + tid] = vsel(ws[it], wok[it] && ok);
+      if (it * 256 + tid < WV) s_w[it * 256 + tid] = vsel(wr[it], wok[it] && cok);
   };
 
   f32x4 acc[NTN][TMW];
@@ -114,41 +112,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
 #pragma unroll
     for (int j = 0; j < TMW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // one LDS buffer, refilled between barriers; the next PF chunks are in registers during the MFMAs
+  // one LDS buffer, refilled between barriers; the next chunk is in registers during the MFMAs (two buffers and
+  // one barrier per chunk measured even or slower: kbench bs16 384->64 @40^2 27.0 vs 26.7 us, 64->128 13.2 vs 15.7)
   const int nchunks = p.Cin / BK;
-#pragma unroll
-  for (int u = 0; u < PF; ++u) load_chunk(u * BK, xr[u], wr[u], cok[u]);
-  store_chunk(xr[0], wr[0], cok[0]);
+  load_chunk(0);
+  store_chunk();
   __syncthreads();
-  for (int ch0 = 0; ch0 < nchunks; ch0 += PF) {
+  for (int ch = 0; ch < nchunks; ++ch) {
+    if (ch + 1 < nchunks) load_chunk((ch + 1) * BK);
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int ch = ch0 + u;
-      if (PF > 1 || ch + 1 < nchunks) load_chunk((ch + PF) * BK, xr[u], wr[u], cok[u]);
-      if (ch < nchunks) {  // uniform
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap % 3;
+      opv af[NTN], bf[TMW];
 #pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int ky = tap / 3, kx = tap % 3;
-          opv af[NTN], bf[TMW];
+      for (int i = 0; i < NTN; ++i) af[i] = s_w[((i * 9 + tap) * 4 + g) * 16 + r16];
 #pragma unroll
-          for (int i = 0; i < NTN; ++i) af[i] = s_w[((i * 9 + tap) * 4 + g) * 16 + r16];
-#pragma unroll
-          for (int j = 0; j < TMW; ++j) {
-            const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
-            bf[j] = s_x[hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
-          }
-#pragma unroll
-          for (int j = 0; j < TMW; ++j)
-#pragma unroll
-            for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
-        }
-        if (ch + 1 < nchunks) {
-          const int nx = (u + 1) % PF;
-          __syncthreads();  // every wave is done reading this chunk
-          store_chunk(xr[nx], wr[nx], cok[nx]);
-          __syncthreads();
-        }
+      for (int j = 0; j < TMW; ++j) {
+        const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
+        bf[j] = s_x[hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
       }
+#pragma unroll
+      for (int j = 0; j < TMW; ++j)
+#pragma unroll
+        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
+    }
+    if (ch + 1 < nchunks) {
+      __syncthreads();  // every wave is done reading this chunk
+      store_chunk();
+      __syncthreads();
     }
   }
 
@@ -167,8 +158,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co);
 }
 
-template <typename T, bool Q8, int S, int TH, int PF>
-static void launch_halo_pf(const ConvArgs<T>& a, hipStream_t s) {
+template <typename T, bool Q8, int S, int TH>
+static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
@@ -177,22 +168,18 @@ static void launch_halo_pf(const ConvArgs<T>& a, hipStream_t s) {
   // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench)
   constexpr int64_t n2_below = 512;
   if (a.Cout <= 32) {
-    conv3x3_halo_kernel<T, S, TH, 2, Q8, PF><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
     const int cs = (int)cdiv(a.Cout, 32);
-    conv3x3_halo_kernel<T, S, TH, 2, Q8, PF><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   } else {
     const int cs = (int)cdiv(a.Cout, 64);
-    conv3x3_halo_kernel<T, S, TH, 4, Q8, PF><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 4, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   }
 }
 
-// One chunk in flight: two or three (the kernel's PF) measured slower on every head shape (kbench bs16, PF 1 / 2 / 3:
-// 384->64 @40^2 26.6 / 28.8 / 31.3 us, 256->32 @80^2 28.4 / 32.8 / 47.1, 64->128 @40^2 12.9 / 17.1 / 19.9)
-template <typename T, bool Q8, int S, int TH>
-static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
-  launch_halo_pf<T, Q8, S, TH, 1>(a, s);
-}
+// (One chunk in flight: a register ring of two or three was slower on every head shape, kbench bs16 1 / 2 / 3
+// chunks: 384->64 @40^2 26.6 / 28.8 / 31.3 us, 256->32 @80^2 28.4 / 32.8 / 47.1, 64->128 @40^2 12.9 / 17.1 / 19.9.)
 
 // 3x3, pad 1, dil 1, stride 1/2, Cin a multiple of BK and >= 2 chunks.  Returns false when the
 // shape is not this kernel's (the caller falls back to the implicit-GEMM kernels).
