@@ -559,7 +559,10 @@ def test_stem2(c0, n, h, w):
     (64, 1, 17, 100, False, 8, 0, 0), (16, 3, 5, 3, True, 16, 8, 0), (32, 2, 40, 48, False, 16, 0, 0),
     (64, 3, 48, 33, True, 16, 16, 0), (16, 1, 1, 1, True, 8, 0, 0), (64, 8, 80, 80, True, 8, 0, 0),
     # c_mid = 64: the Detect box branch Conv(64,64,3) -> Conv(64,64,3) (head.py:86-90)
-    (64, 2, 80, 80, False, 0, 0, 64), (64, 3, 37, 29, False, 8, 8, 64), (64, 1, 5, 3, True, 0, 0, 64)])
+    (64, 2, 80, 80, False, 0, 0, 64), (64, 3, 37, 29, False, 8, 8, 64), (64, 1, 5, 3, True, 0, 0, 64),
+    # more tiles than resident workgroups (ragged maps, channel slices): several tiles per workgroup wherever the
+    # walk is persistent
+    (16, 4, 320, 320, True, 16, 8, 0), (32, 3, 165, 158, True, 0, 0, 0), (16, 2, 331, 318, False, 0, 8, 0)])
 def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra, cm):
     """ydbl_bottleneck_nhwc (cv1 3x3 c->c_mid, cv2 3x3 c_mid->c, SiLU, optional x + ..., fp16) vs the two
     convs in fp32 on fp16-rounded operands, the intermediate rounded to fp16 as the unfused path stores it
