@@ -260,6 +260,13 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
     const unsigned char* inb = reinterpret_cast<const unsigned char*>(in);
     auto conv1 = [&](auto interior_c) {
       constexpr bool INTERIOR = decltype(interior_c)::value;
+      // this lane's output pixel p = pt * 16 * PS + 16 * my_set + r16 of the virtual grid, its (row, column) and
+      // record row base walked incrementally (one division before the loop, none in it)
+      constexpr int STEP = 4 * 16 * PS, DR = STEP / Cfg::INW, DC = STEP % Cfg::INW;
+      static_assert(STEP < 2 * Cfg::INW, "one row wrap per step at most");
+      int p = wave * 16 * PS + my_set * 16 + r16;
+      int lr = p / Cfg::INW, lc = p - lr * Cfg::INW;
+      int rb = lr * 2 * Cfg::L0P;
       for (int pt = wave; pt * 16 * PS < P0V; pt += 4) {
         const int p0 = pt * 16 * PS + r16;
         f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -270,24 +277,31 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
           const h8 bf = h8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
           acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[m], bf, acc, 0, 0, 0);
         }
-        const int p = p0 + my_set * 16;
-        const int lr = p / Cfg::INW, lc = p - lr * Cfg::INW;
-        if (p >= P0V || lc >= Cfg::L0W) continue;
-        h4 hv;
-        if constexpr (INTERIOR) {
+        if (p < P0V && lc < Cfg::L0W) {
+          h4 hv;
+          if constexpr (INTERIOR) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) hv[q] = f16_rne(silu_fast(acc[q]));
-        } else {
-          const int iy = tl.Y0 + lr, ix = tl.X0 + lc;
-          const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
+            for (int q = 0; q < 4; ++q) hv[q] = f16_rne(silu_fast(acc[q]));
+          } else {
+            const int iy = tl.Y0 + lr, ix = tl.X0 + lc;
+            const bool inside = iy >= 0 && iy < H && ix >= 0 && ix < W;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const float sv = silu_fast(acc[q]);
-            hv[q] = f16_rne(inside ? sv : 0.f);
+            for (int q = 0; q < 4; ++q) {
+              const float sv = silu_fast(acc[q]);
+              hv[q] = f16_rne(inside ? sv : 0.f);
+            }
           }
+          const int rec = rb + (lc & 1) * Cfg::L0P + (lc >> 1);
+          *reinterpret_cast<h4*>(l0w + rec * 16) = hv;
         }
-        const int rec = lr * 2 * Cfg::L0P + (lc & 1) * Cfg::L0P + (lc >> 1);
-        *reinterpret_cast<h4*>(l0w + rec * 16) = hv;
+        p += STEP;
+        lc += DC;
+        lr += DR;
+        rb += DR * 2 * Cfg::L0P;
+        const bool wrap = lc >= Cfg::INW;
+        lc -= wrap ? Cfg::INW : 0;
+        lr += wrap ? 1 : 0;
+        rb += wrap ? 2 * Cfg::L0P : 0;
       }
     };
     if (interior) conv1(std::true_type{});
