@@ -54,10 +54,12 @@ def build_library(force: bool = False, jobs: int | None = None) -> Path:
             list(ex.map(lambda a: _compile(*a), todo))
     newest = max(o.stat().st_mtime for o in objs)
     if force or todo or not LIB_PATH.exists() or LIB_PATH.stat().st_mtime < newest:
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(LIB_PATH)]
+        tmp = LIB_PATH.with_name(LIB_PATH.name + ".tmp")  # linked aside, then renamed: never a half-written library
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+        os.replace(tmp, LIB_PATH)
     return LIB_PATH
 
 
