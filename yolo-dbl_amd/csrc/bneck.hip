@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
   unsigned char* s_in = smem;                    // [CH][PIN] records
   unsigned char* s_mid = smem + Cfg::IN_BYTES;   // [CHM][PMID] records
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = wave_id();
   const int g = lane >> 4, r16 = lane & 15;
   BN_STAMP(0);
 #ifdef YDBL_BNECK_STAMPS
@@ -218,8 +218,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
   // ---- 2. cv1 over the virtual grid: MR rows x IP columns, mid pixel v reads input record v + tap.
   // Two 16-pixel groups per iteration (independent accumulators: the LDS reads of one overlap the
   // MFMAs of the other, and the two SiLU epilogues interleave)
-  auto epi1 = [&](const f32x4& acc, int v) {
-    const int vr = v / IP, vc = v - vr * IP;
+  auto epi1 = [&](const f32x4& acc, int vr, int vc, int rb) {
     if (vr >= Cfg::MR || c1 >= CM) return;
     bool inside = true;
     if (!interior) {
@@ -228,10 +227,23 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     }
     h4 o;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = f16_rne(inside ? silu_fast(acc[q] + bias1[q]) : 0.f);
-    *reinterpret_cast<h4*>(mid_w + (vr * MP + vc) * 16) = o;
+    for (int q = 0; q < 4; ++q) {
+      const float sv = silu_fast(acc[q] + bias1[q]);  // computed unconditionally: a select, not a branch per value
+      o[q] = f16_rne(inside ? sv : 0.f);
+    }
+    *reinterpret_cast<h4*>(mid_w + (rb + vc) * 16) = o;
   };
   constexpr int WPT1 = 4 / NT1;
+  // the two groups' virtual-grid (row, column) and intermediate row base, walked incrementally (no division
+  // or 32-bit multiply in the loop): group 0 advances S0 pixels per iteration, group 1 sits H1 pixels after it
+  constexpr int S0 = 2 * WPT1 * 16, H1 = WPT1 * 16;
+  int r0, c0, rb0;
+  {
+    const int v = (wave / NT1) * 16 + r16;
+    r0 = v / IP;
+    c0 = v - r0 * IP;
+    rb0 = r0 * MP;
+  }
   for (int gi = wave / NT1; gi < Cfg::G1; gi += 2 * WPT1) {
     const int v0 = gi * 16 + r16;
     const bool two = gi + WPT1 < Cfg::G1;  // wave-uniform
@@ -247,8 +259,17 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
       acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf0, acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf1, acc1, 0, 0, 0);
     }
-    epi1(acc0, v0);
-    if (two) epi1(acc1, v1);
+    epi1(acc0, r0, c0, rb0);
+    if (two) {
+      const bool w1 = c0 + H1 % IP >= IP;
+      const int dr = H1 / IP + (w1 ? 1 : 0);
+      epi1(acc1, r0 + dr, c0 + H1 % IP - (w1 ? IP : 0), rb0 + dr * MP);
+    }
+    const bool w0 = c0 + S0 % IP >= IP;
+    const int dr = S0 / IP + (w0 ? 1 : 0);
+    c0 += S0 % IP - (w0 ? IP : 0);
+    r0 += dr;
+    rb0 += dr * MP;
   }
 
   const unsigned char* res_r = s_in + ((c2 >> 3) * PIN + 2 * IP + 2) * 16 + (c2 & 7) * 2;
@@ -261,6 +282,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
   BN_STAMP(2);
 
   // ---- 3. cv2: output rows j, j + WPT2 of the tile, 16 columns = the 16 lanes
+  const int64_t lane_px = (int64_t)r16 * y.cs;  // this lane's pixel offset from the row's first column
   auto epi2 = [&](const f32x4& acc, int j) {
     const int oy = oy0 + j, ox = ox0 + r16;
     if (oy >= y.h || ox >= y.w) return;
@@ -278,7 +300,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
       for (int q = 0; q < 4; ++q) o[q] = f16_rne(v[q]);
       *reinterpret_cast<h4*>(s_in + ((c2 >> 3) * (TH * 16) + j * 16 + r16) * 16 + (c2 & 7) * 2) = o;
     } else {
-      store_f<4>(y.at(img, oy, ox) + c2, v);
+      store_f<4>(y.at(img, oy, ox0) + lane_px + c2, v);  // row base wave-uniform (scalar address arithmetic)
     }
   };
   constexpr int WPT2 = 4 / NT2;

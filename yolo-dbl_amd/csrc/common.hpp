@@ -66,6 +66,10 @@ __device__ __forceinline__ int xcd_remap(int b, int n) {
   return (b & 7) * (n >> 3) + (b >> 3);
 }
 
+// This lane's wave within the workgroup, as a scalar: hipcc's divergence analysis treats threadIdx.x >> 6 as
+// per-lane, which puts every loop over a wave's share of the work (and its exec-mask bookkeeping) on the VALU.
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
 // Unconditional load + select: `ok ? *p : 0` without a branch around the load.  hipcc turns a
 // per-lane "load or zero" into a branch with its own s_waitcnt vmcnt(0), which serialises every
 // load of an unrolled staging loop; loading from a clamped, always-valid address and selecting

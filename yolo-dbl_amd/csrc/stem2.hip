@@ -192,7 +192,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
     }
   };
 
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = wave_id();
   const int g = lane >> 4, r16 = lane & 15;
 
   // First conv over a virtual grid of L0H rows x INW columns (the input tile's pitch; the last two
@@ -311,6 +311,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
 
     // ---- 3. second conv: TH rows x TW cols, 16-pixel row segments
     constexpr int SEG = TW / 16;
+    const int64_t lane_px = (int64_t)r16 * y.cs;
     for (int st = wave; st < TH * SEG; st += 4) {
       const int j = st / SEG, i = (st - j * SEG) * 16 + r16;
       const unsigned char* pbase = l0 + ((2 * j) * 2 * Cfg::L0P + i) * 16;
@@ -325,7 +326,8 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
       }
       const int oy = tl.oy0 + j, ox = tl.ox0 + i;
       if (oy >= y.h || ox >= y.w) continue;
-      _Float16* yp = y.at(tl.img, oy, ox);
+      // segment base wave-uniform (scalar address arithmetic) + this lane's pixel
+      _Float16* yp = y.at(tl.img, oy, tl.ox0 + (st - j * SEG) * 16) + lane_px;
 #pragma unroll
       for (int q = 0; q < Cfg::NT1; ++q) {
         float o[4];
