@@ -18,7 +18,7 @@ else
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $T/prof_s1 -o run -- python bench.py --streams 1 --steps 20 --warmup 5 \
       --no-cpu-baseline > $T/prof_s1.log 2>&1 || { echo "single-stream rocprof failed"; tail -20 $T/prof_s1.log; exit 1; }
   python scripts/rocpd_stats.py $T/prof_s1/run_results.db > $T/c2_streams1_kernel_stats.csv
-  tail -1 $T/prof_s1.log > $T/c2_streams1_bench.json
+  grep "^{\"metric\"" $T/prof_s1.log | tail -1 > $T/c2_streams1_bench.json
   python scripts/rocprof_families.py $T/c2_streams1_kernel_stats.csv $T/c2_streams1_bench.json > $T/roofline_vs_rocprof.txt 2>&1; cat $T/roofline_vs_rocprof.txt | head -20
   bash scripts/pmc_families.sh ${1:-r04rec}_pmc $T/r04_pmc_families.json --streams 1
 fi
