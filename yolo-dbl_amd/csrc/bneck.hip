@@ -59,7 +59,11 @@ template <int C, int CMID, int TH, int CIN = C>
 struct BneckCfg {
   static constexpr int CM = CMID, CH = CIN / 8, CHM = (CM + 7) / 8;  // CH: 8-channel chunks of the input
   static constexpr int NT1 = (CM + 15) / 16, NT2 = C / 16;
-  static constexpr int KS1 = ksteps<CH>(), KS2 = ksteps<CHM>();
+  // BD (8-channel intermediate of a 16-channel input): cv1's 16 MFMA rows are two pixel sets x 8 channels through a
+  // block-diagonal A (rows 0-7 see set 0's K slots, rows 8-15 set 1's), so no D row is dead; k-step m = tap m,
+  // lane group g = (set g / 2, chunk g % 2)
+  static constexpr bool BD = CM == 8 && CH == 2;
+  static constexpr int KS1 = BD ? 9 : ksteps<CH>(), KS2 = ksteps<CHM>();
   static constexpr int TW = 16;
   static constexpr int IP = TW + 4;                  // input window pitch (records) = its width
   static constexpr int IR = TH + 5;                  // + 1 slack row for the virtual grid's tail
@@ -87,6 +91,15 @@ void bneck_pack(const float* w1, const float* b1, const float* w2, const float* 
   _Float16* f2 = f1 + Cfg::W1F * 8;
   float* fb1 = reinterpret_cast<float*>(f2 + Cfg::W2F * 8);
   float* fb2 = fb1 + Cfg::NT1 * 16;
+  if constexpr (Cfg::BD) {
+    for (int m = 0; m < Cfg::KS1; ++m)
+      for (int lane = 0; lane < 64; ++lane)
+        for (int j = 0; j < 8; ++j) {
+          const int g = lane >> 4, row = lane & 15;
+          const int co = row % 8, ci = (g & 1) * 8 + j;
+          f1[(m * 64 + lane) * 8 + j] = (_Float16)((row / 8) == (g >> 1) ? w1[(co * CIN + ci) * 9 + m] : 0.f);
+        }
+  } else
   for (int t = 0; t < Cfg::NT1; ++t)
     for (int m = 0; m < Cfg::KS1; ++m)
       for (int lane = 0; lane < 64; ++lane)
@@ -202,7 +215,7 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
   for (int u = 0; u < IT; ++u)
     if (px0 + u * PXU < Cfg::NPX) *reinterpret_cast<h8*>(s_dst + u * PXU * 16) = xr[u];
   float bias1[4], bias2[4];
-  const int c1 = 16 * t1 + 4 * g;  // first intermediate channel of this lane's cv1 D rows
+  const int c1 = Cfg::BD ? 4 * (g & 1) : 16 * t1 + 4 * g;  // first intermediate channel of this lane's cv1 D rows
   const int c2 = 16 * t2 + 4 * g;  // first output channel of this lane's cv2 D rows
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -248,22 +261,39 @@ __global__ __launch_bounds__(256, 2) void bneck_kernel(DView<const _Float16> x, 
     const int v0 = gi * 16 + r16;
     const bool two = gi + WPT1 < Cfg::G1;  // wave-uniform
     const int v1 = two ? v0 + 16 * WPT1 : v0;
-    f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    const unsigned char* p0 = in_b + v0 * 16;
-    const unsigned char* p1 = in_b + v1 * 16;
+    if constexpr (Cfg::BD) {
+      // one accumulator for both groups: lane group g reads set g / 2's pixel, chunk g % 2, at tap m
+      const int set = g >> 1;
+      const unsigned char* pb = s_in + ((g & 1) * PIN + (set ? v1 : v0)) * 16;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int m = 0; m < KS1; ++m) {
-      const int o = koff<CH, PIN, IP>(m, g);
-      const h8 bf0 = *reinterpret_cast<const h8*>(p0 + o);
-      const h8 bf1 = *reinterpret_cast<const h8*>(p1 + o);
-      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf0, acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf1, acc1, 0, 0, 0);
-    }
-    epi1(acc0, r0, c0, rb0);
-    if (two) {
+      for (int m = 0; m < KS1; ++m) {
+        const h8 bf = *reinterpret_cast<const h8*>(pb + ((m / 3) * IP + m % 3) * 16);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf, acc, 0, 0, 0);
+      }
+      // one epilogue for both sets (per-lane position select, not a branch per set); set 1 of a single-group
+      // iteration duplicates group 0 and is skipped through an out-of-range row
       const bool w1 = c0 + H1 % IP >= IP;
-      const int dr = H1 / IP + (w1 ? 1 : 0);
-      epi1(acc1, r0 + dr, c0 + H1 % IP - (w1 ? IP : 0), rb0 + dr * MP);
+      const int dr = set ? H1 / IP + (w1 ? 1 : 0) : 0;
+      epi1(acc, set && !two ? Cfg::MR : r0 + dr, set ? c0 + H1 % IP - (w1 ? IP : 0) : c0, rb0 + dr * MP);
+    } else {
+      f32x4 acc0 = f32x4{0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+      const unsigned char* p0 = in_b + v0 * 16;
+      const unsigned char* p1 = in_b + v1 * 16;
+#pragma unroll
+      for (int m = 0; m < KS1; ++m) {
+        const int o = koff<CH, PIN, IP>(m, g);
+        const h8 bf0 = *reinterpret_cast<const h8*>(p0 + o);
+        const h8 bf1 = *reinterpret_cast<const h8*>(p1 + o);
+        acc0 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf0, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[m], bf1, acc1, 0, 0, 0);
+      }
+      epi1(acc0, r0, c0, rb0);
+      if (two) {
+        const bool w1 = c0 + H1 % IP >= IP;
+        const int dr = H1 / IP + (w1 ? 1 : 0);
+        epi1(acc1, r0 + dr, c0 + H1 % IP - (w1 ? IP : 0), rb0 + dr * MP);
+      }
     }
     const bool w0 = c0 + S0 % IP >= IP;
     const int dr = S0 / IP + (w0 ? 1 : 0);
