@@ -56,11 +56,17 @@ __device__ __forceinline__ bool class_ok(int j, const int* classes, int ncls) {
   return false;
 }
 
+// Four lanes per anchor (a quad): lane s computes side s's DFL expectation (16 bins; the quad's four sides are
+// then shared by shuffles) and the classes j = s, s + 4, ...; so a lane's dependent chain is 16 exponentials
+// instead of 64, and the launch has four times the waves to hide it.  Same arithmetic per value as one lane per
+// anchor: the decoded boxes, scores and candidate sets are unchanged (candidate order within an image may differ;
+// every candidate carries its anchor / class index).
 template <typename T>
 __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
   const int b = blockIdx.y;
-  const int a = blockIdx.x * blockDim.x + threadIdx.x;
-  if (a >= p.A) return;
+  const int tq = blockIdx.x * blockDim.x + threadIdx.x;
+  const int a = tq >> 2, s = tq & 3;
+  if (a >= p.A) return;  // whole quads
   int l = 0;
   while (l < p.nl - 1 && a >= p.a_end[l]) ++l;
   const int a0 = l ? p.a_end[l - 1] : 0;
@@ -68,9 +74,8 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
   const DView<const T>& bx = p.box[l];
   const int gx = loc % bx.w, gy = loc / bx.w;
   const T* bp = bx.at(b, gy, gx);
-  float dist[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {  // DFL: softmax over 16 bins, expectation with weights 0..15
+  float mine;
+  {  // DFL: softmax over 16 bins, expectation with weights 0..15
     float v[16];
     load_f<8>(bp + s * 16, v);
     load_f<8>(bp + s * 16 + 8, v + 8);
@@ -89,8 +94,12 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) acc += float(k) * (e[k] * inv);
-    dist[s] = acc;
+    mine = acc;
   }
+  const int q0 = (threadIdx.x & 63) & ~3;  // the quad's first lane
+  float dist[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dist[k] = __shfl(mine, q0 + k);
   const float ax = float(gx) + 0.5f, ay = float(gy) + 0.5f, st = p.stride[l];
   const float x1 = ax - dist[0], y1 = ay - dist[1], x2 = ax + dist[2], y2 = ay + dist[3];
   const float cx = ((x1 + x2) / 2.0f) * st, cy = ((y1 + y2) / 2.0f) * st;
@@ -98,7 +107,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
   const int64_t A = p.A;
   if (p.yref) {
     float* yr = p.yref + (int64_t)b * (4 + p.nc) * A + a;
-    yr[0] = cx; yr[A] = cy; yr[2 * A] = w; yr[3 * A] = h;
+    yr[s * A] = s == 0 ? cx : s == 1 ? cy : s == 2 ? w : h;
   }
   // xywh2xyxy (U/utils/ops.py:416-433)
   const float hw = w / 2.0f, hh = h / 2.0f;
@@ -106,7 +115,7 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
   const T* cp = p.cls[l].at(b, gy, gx);
   float best = -1.f;
   int bj = 0;
-  for (int j = 0; j < p.nc; ++j) {
+  for (int j = s; j < p.nc; j += 4) {
     const float sc = 1.0f / (1.0f + expf(-float(cp[j])));
     if (p.yref) p.yref[((int64_t)b * (4 + p.nc) + 4 + j) * A + a] = sc;
     if (p.multi) {
@@ -118,12 +127,23 @@ __global__ __launch_bounds__(256) void decode_kernel(DecodeArgs<T> p) {
           p.cscore[o] = sc; p.ccls[o] = j; p.cidx[o] = a * p.nc + j;
         }
       }
-    } else if (sc > best) {  // torch.max: first index of the maximum
+    } else if (sc > best) {  // torch.max: first index of the maximum (within this lane's classes)
       best = sc;
       bj = j;
     }
   }
-  const int slot = p.multi ? -1 : wave_slot(p.ccount + b, best > p.conf && class_ok(bj, p.classes, p.ncls));
+  if (p.multi) return;
+  // the quad's first maximum: larger score, or the same score at a smaller class index
+#pragma unroll
+  for (int k = 1; k < 4; k <<= 1) {
+    const float ob = __shfl_xor(best, k);
+    const int oj = __shfl_xor(bj, k);
+    if (ob > best || (ob == best && oj < bj)) {
+      best = ob;
+      bj = oj;
+    }
+  }
+  const int slot = wave_slot(p.ccount + b, s == 0 && best > p.conf && class_ok(bj, p.classes, p.ncls));
   if (slot >= 0) {
     if (slot < p.cap) {
       const int64_t o = (int64_t)b * p.cap + slot;
@@ -964,7 +984,7 @@ static int decode_t(const ydbl_decode_desc* d, hipStream_t s) {
   a.cap = d->cap;
   const int B = d->box[0].n;
   zero_counts_kernel<<<1, 256, 0, s>>>(d->cand_count, B);
-  decode_kernel<T><<<dim3((unsigned)cdiv(A, 256), B), 256, 0, s>>>(a);
+  decode_kernel<T><<<dim3((unsigned)cdiv((int64_t)A * 4, 256), B), 256, 0, s>>>(a);  // a quad per anchor
   return check_launch("ydbl_detect_decode");
 }
 
