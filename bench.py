@@ -436,7 +436,7 @@ def main():
                     help="e4m3 dense-conv operands (BASELINE config 5); FRACTION < 1 switches that share of the "
                          "candidate MACs, least output-sensitive convs first (ydbl.quant.enable_fp8)")
     ap.add_argument("--streams", type=int, default=2,
-                    help="sub-batch graphs replayed concurrently on this many HIP streams (DetectSession); "
+                    help="sub-batch plans run concurrently, as branches of one hipGraph (DetectSession); "
                          "2 measured +3 %% DBL-n bs32, +9 %% DBL-s bs64, +8.5 %% DBL-l 1280 bs8 over 1 (4: -33 %% DBL-n)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -483,7 +483,7 @@ def main():
     sp.load(images_local=blob_images(B, S, seed=1234 + rank).to(dev))
 
     def step():
-        sp.run()  # forward + decode + NMS (one hipGraph replay per sub-batch stream) [+ the one all-gather]
+        sp.run()  # forward + decode + NMS (one hipGraph replay, the sub-batch plans as its branches) [+ the one all-gather]
 
     el = timed_steps(step, args, world, lambda: torch.cuda.synchronize(dev), dev)
     key = workload_key(args, dtype_name)

@@ -15,15 +15,16 @@ import torch
 
 from .. import _lib
 from .._lib import DecodeDesc, NmsDesc, View
-from ..runtime import GraphRunner, Plan
+from ..runtime import BranchGraphRunner, GraphRunner, Plan
 
 
 class DetectSession:
     """streams = k > 1: the batch is split into k contiguous sub-batches, each compiled into its own launch
-    plan (own buffers, own hipGraph) and replayed on its own HIP stream, writing into slices of the shared
-    det / count (/ pred) outputs.  At DBL-n/s sizes every launch is short and ramp/tail-bound, so two
-    concurrent half-batch graphs fill each other's gaps (scripts/stream_probe.py: DBL-n bs32 +10 %,
-    DBL-s bs64 +14 %)."""
+    plan (own buffers) writing into slices of the shared det / count (/ pred) outputs; the k plans are captured
+    as k independent branches of ONE hipGraph (runtime.BranchGraphRunner; eager mode: one HIP stream per plan).
+    At DBL-n/s sizes every launch is short and ramp/tail-bound, so two concurrent half-batch branches fill each
+    other's gaps (scripts/stream_probe.py: DBL-n bs32 +10 %, DBL-s bs64 +14 %; one two-branch graph instead of
+    two graphs on two streams a further +2.5 %, scripts/graph_branch_probe.py)."""
 
     def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
                  multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
@@ -128,6 +129,7 @@ class DetectSession:
         self.plans = [c.plan for c in self.children]
         self.plan = self.plans[0]
         self.use_graph = use_graph
+        self._graph = None  # all sub-batch plans as branches of one hipGraph (runtime.BranchGraphRunner)
         self.nc, self.A = self.children[0].nc, self.children[0].A
 
     @property
@@ -178,6 +180,7 @@ class DetectSession:
         for c in owners:
             c._graph = None  # descriptors changed: recapture
             c.fp8_ready = True
+        self._graph = None
         self.fp8_ready = True
         return n
 
@@ -189,7 +192,12 @@ class DetectSession:
     def launch(self):
         if self.fp8 and not self.fp8_ready:
             self.calibrate_fp8()  # first batch calibrates (dynamic post-training quantization)
-        if self.children:  # fork: each sub-batch's graph on its own stream, then join
+        if self.children and self.use_graph:  # every sub-batch plan a branch of one graph: one launch
+            if self._graph is None:
+                self._graph = BranchGraphRunner(self.plans)
+            self._graph.replay()
+            return
+        if self.children:  # eager: each sub-batch plan on its own stream, then join
             cur = torch.cuda.current_stream(self.det.device)
             for c, st in zip(self.children, self.streams):
                 st.wait_stream(cur)
