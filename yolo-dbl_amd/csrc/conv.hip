@@ -530,6 +530,15 @@ static bool try_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
   if (!(a.K >= 1024 || (a.K >= 512 && a.P <= 16384))) return false;
   auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
   const int64_t want = 768;
+  // Under 256 workgroups with the tiles below (the 20^2 maps of a bs16 sub-batch): half-height tiles, 16 pixels
+  // for Cout <= 64 and 64-wide columns for Cout 128 -- twice the workgroups for the same k-loop (bs16 graphs:
+  // 128->128 3x3 s2 @20^2 17.4 -> 14.4 us, 64->64 3x3 @20^2 9.5 -> 8.6, 256->64 18.4 -> 17.7; DBL-n bs32 even to
+  // +0.5 % over two boxes, DBL-s bs64 even: profiles/r04/r04_wsk_small_tiles_ab.txt)
+  if (a.Cout <= 128 && blocks(32, a.Cout <= 64 ? 64 : 128) < 256) {
+    if (a.Cout <= 64) launch_wsk<T, Q8, 16, 64>(a, pointwise, s);
+    else launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
+    return true;
+  }
   if (a.Cout <= 32) {
     if (blocks(128, 32) >= want) { launch_wsk<T, Q8, 128, 32>(a, pointwise, s); return true; }
     launch_wsk<T, Q8, 64, 32>(a, pointwise, s);
