@@ -438,6 +438,10 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="sub-batch plans run concurrently, as branches of one hipGraph (DetectSession); "
                          "2 measured +3 %% DBL-n bs32, +9 %% DBL-s bs64, +8.5 %% DBL-l 1280 bs8 over 1 (4: -33 %% DBL-n)")
+    ap.add_argument("--via-predict", action="store_true",
+                    help="time the public API instead of the session: each step is YOLO.predict(batch, half=...) on "
+                         "the HBM-resident batch (LoadTensor checks + copy into the session's input buffer, the "
+                         "same split hipGraph, the per-batch count sync, Results objects); no roofline / CPU legs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stub-cpu", action="store_true", help="gloo/CPU plumbing check of the N-rank launch (no GPU)")
@@ -474,6 +478,8 @@ def main():
 
     # this rank's B images of the global batch B * world; its NMS writes the per-image [det | count] records
     # that the step's one all-gather ships (ydbl.parallel; no process group at N = 1: no collective)
+    if args.via_predict:
+        return predict_main(args, model, world, rank, dev, half, fp8, dtype_name, cfg)
     sp = ShardedPredictor(model, B * world, S, S, dev, half=half, conf=0.25, iou=0.7, max_det=300, fp8=fp8,
                           streams=args.streams)
     sess = sp.session
@@ -514,6 +520,35 @@ def main():
         cpu = cpu_baseline(args.model, S, B, gpu_session=(model, fp8, half))
     if rank == 0:
         emit_line(args, world, el, dtype_name, cfg, extra, rf, cpu)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def predict_main(args, model, world, rank, dev, half, fp8, dtype_name, cfg):
+    """--via-predict: the step is the user-facing call YOLO.predict(x, half=...) on this rank's HBM-resident
+    batch, with predict()'s own stream layout (ydbl.engine.session.default_streams: the split hipGraph from
+    batch 4 up); the line says so in config.via."""
+    from ydbl.utils.synthetic import blob_images
+
+    B, S = args.batch, args.imgsz
+    x = blob_images(B, S, seed=1234 + rank).to(dev)
+    kw = dict(half=half, fp8=fp8, conf=0.25, iou=0.7, max_det=300, device=dev)
+    if fp8:  # calibrate once on the separate synthetic batch, as the session bench does
+        from ydbl.engine.session import default_streams
+
+        model.session(B, S, S, half=True, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=fp8,
+                      streams=default_streams(B)).calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
+    out = {}
+
+    def step():
+        out["r"] = model.predict(x, **kw)
+
+    el = timed_steps(step, args, world, lambda: torch.cuda.synchronize(dev), dev)
+    if rank == 0:
+        extra = {"dets_per_image": round(sum(len(r.boxes.data) for r in out["r"]) / B, 2),
+                 "via": "YOLO.predict(x, half=%s) per step (Results construction and one count sync included)"
+                        % half}
+        emit_line(args, world, el, dtype_name, cfg, extra, None, None)
     if world > 1:
         dist.destroy_process_group()
 

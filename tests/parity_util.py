@@ -64,15 +64,23 @@ def fp32_rule(st):
     return 2 * st["box_max"] + 1e-3, 2 * st["conf_max"] + 1e-6
 
 
-def fp32_rule_max(st):
-    """The value bound of the fp32 comparison: the worst and the p99.9 deviation from fp64 each within three
-    times the reference fp32 path's own (+ the floor).  Both paths are fp32 and differ in summation order (and
-    expf), so their deviations are of one order but not ordered: measured GPU / reference-fp32 ratios (max, p99.9)
-    on the pinned images are DBL-s bs32 box 1.43x / 1.47x, score 2.04x / 1.62x and DBL-x bs2 (a fixture ~50x
-    worse conditioned) box 1.47x / 2.26x, score 1.66x / 2.02x.
-    Returns (box max, score max, box p99.9, score p99.9)."""
-    return (3 * st["box_max"] + 1e-3, 3 * st["conf_max"] + 1e-6, 3 * st["box_p999"] + 1e-4,
-            3 * st["conf_p999"] + 1e-7)
+# fp32 value-bound factors per fixture (max, p99.9): the GPU's deviation from fp64 / the oracle fp32 leg's.  Both paths
+# are fp32 and differ in summation order (and expf), so their deviations are of one order but not ordered; the factor
+# is 2 except where a pinned layout measured above it (round 5, every layout of tests/test_gpu_e2e.py, max / p99.9):
+# n640 1.40 / 1.27, s640 box 2.01 (bs8 as two bs4 graphs) and score 2.07 (bs32) / 1.63, l1280 1.65 / 1.71, x640 (a
+# fixture ~50x worse conditioned, not a BASELINE model) 1.66 / 2.26
+FP32_FACTOR = {"n": (2.0, 2.0), "s": (2.5, 2.0), "l": (2.0, 2.0), "x": (2.0, 3.0)}
+# NMS decisions within the tolerance of flipping, beyond twice the reference fp32 path's own count (a count of rare
+# events; measured round 5: s640 bs32 one graph 2, every other fixture / layout 0 beyond the reference's)
+FP32_BORDERLINE_EXTRA = {"n": 0, "s": 2, "l": 0, "x": 0}
+
+
+def fp32_rule_max(st, scale):
+    """The value bound of the fp32 comparison: the worst and the p99.9 deviation from fp64 each within FP32_FACTOR
+    times the reference fp32 path's own (+ the floor).  Returns (box max, score max, box p99.9, score p99.9)."""
+    fm, fp = FP32_FACTOR[scale]
+    return (fm * st["box_max"] + 1e-3, fm * st["conf_max"] + 1e-6, fp * st["box_p999"] + 1e-4,
+            fp * st["conf_p999"] + 1e-7)
 
 
 def fp16_rule(st):
@@ -94,6 +102,41 @@ def load_e2e(golden_dir, name):
         if "d32" in z.files:
             meta["y32"] = y64 + torch.from_numpy(z["d32"]).double()
         return y64, meta
+
+
+def batch_images(meta, batch, streams=1):
+    """Indices (into the fixture's full synthetic batch) of a `batch`-image test batch that puts the fixture's
+    reference images into EVERY sub-batch graph of a streams-way split session (DetectSession: contiguous
+    ydbl.parallel.shard_bounds slices): the reference images are dealt to the sub-batches in order, each group
+    at the start of its sub-batch with its last image at the sub-batch's end (where the flattened-pixel kernels
+    put their ragged last tile); the other positions take the remaining images in order.  A full batch that
+    already has reference images in every sub-batch graph is returned unchanged.  Images are independent through
+    the network, so a position change is only a routing change (the kernels' tile / workgroup choice depends on
+    the sub-batch size, not on the images)."""
+    from ydbl.parallel import shard_bounds
+
+    full, ref = meta["batch_full"], list(meta["ref_images"])
+    if batch > full:
+        raise ValueError(f"batch {batch} > the fixture's {full}")
+    bounds = [shard_bounds(batch, streams, r) for r in range(streams)] if streams > 1 else [(0, batch)]
+    if batch == full and all(any(a <= i < b for i in ref) for a, b in bounds):
+        return list(range(full))  # the full batch already has reference images in every sub-batch graph
+    ref = ref[:batch]
+    n = len(bounds)
+    groups = [ref[len(ref) * i // n: len(ref) * (i + 1) // n] for i in range(n)]
+    pos = [None] * batch
+    for (a, b), g in zip(bounds, groups):
+        g = g[: b - a]
+        if not g:
+            continue
+        pos[a] = g[0]
+        if len(g) > 1:
+            pos[b - 1] = g[-1]
+        for k, im in enumerate(g[1:-1]):
+            pos[a + 1 + k] = im
+    placed = {p for p in pos if p is not None}
+    fill = iter(i for i in range(full) if i not in placed)
+    return [p if p is not None else next(fill) for p in pos]
 
 
 def direct_report(yg, meta):

@@ -137,6 +137,33 @@ def test_predict_api(golden_dir):
     assert torch.equal(r255[0].boxes.data, res[0].boxes.data)
 
 
+def test_predict_runs_benched_layout(golden_dir):
+    """predict() builds the session layout bench.py times (ydbl.engine.session.default_streams: two sub-batch
+    branches of one hipGraph from batch 4 up), and its detections are bit-equal to that session's
+    (U/engine/model.py:501-560 is the reference's predict)."""
+    from ydbl.engine.session import default_streams
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    assert default_streams(32) == 2 and default_streams(3) == 1
+    x = blob_images(32, 640, seed=1234).cuda()
+    res = p.predict(x, half=True)
+    used = list(p._sessions.values())[-1]
+    assert len(used.children) == 2 and [c.batch for c in used.children] == [16, 16]
+    ref = p.session(32, 640, 640, half=True, conf=0.25, iou=0.7, streams=2, keep_pred=False)
+    assert ref is used  # the very session the bench layout compiles (same cache key)
+    other = p._sessions.copy()
+    p._sessions.clear()
+    d2, c2 = (t.clone() for t in p.session(32, 640, 640, half=True, streams=2)(x))
+    p._sessions.update(other)
+    torch.cuda.synchronize()
+    assert sum(len(r.boxes.data) for r in res) > 0
+    for i, r in enumerate(res):
+        assert torch.equal(r.boxes.data, d2[i, : int(c2[i])])
+    res3 = p.predict(x[:3], half=True)  # below SPLIT_MIN_BATCH: one graph
+    assert len(list(p._sessions.values())[-1].children) == 0 and len(res3) == 3
+
+
 def _cpu_map50(o, x, labels, conf=0.001):
     """mAP@0.5 of the CPU oracle path under the same val protocol (multi-label NMS, conf .001)."""
     from oracle.ops import clip_boxes, non_max_suppression
@@ -354,25 +381,37 @@ def test_detection_model_forward(golden_dir, half):
 def test_sharded_predictor_nccl_world1(golden_dir, tmp_path):
     """The batch-sharded path with its one collective on RCCL: a world-size-1 "nccl" process group (FileStore), a
     ShardedPredictor over DBL-n bs4 at 640 whose NMS writes the [det | count] records and whose all_gather_into_tensor
-    runs on RCCL; the gathered global detections are bit-equal to the plain session's (U/engine/trainer.py:222-227
-    is the reference's process-group setup)."""
+    runs on RCCL.  The batch holds the e2e fixture's reference images in both sub-batch graphs
+    (parity_util.batch_images); the gathered global detections are bit-equal to the plain session's AND, on the
+    reference images, agree with the oracle's fp64 answer under the fp16 rule of tests/test_gpu_e2e.py
+    (U/engine/trainer.py:222-227 is the reference's process-group setup)."""
     import torch.distributed as dist
 
+    from parity_util import batch_images, detections, err_stats, fp16_rule, load_e2e, match_detections
     from ydbl.parallel import ShardedPredictor
     from ydbl.utils.synthetic import blob_images
 
     p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
-    x = blob_images(4, 640, seed=11).cuda()
+    y64_all, meta = load_e2e(golden_dir, "n640")
+    idx = batch_images(meta, 4, 2)
+    pos = [k for k, i in enumerate(idx) if i in meta["ref_images"]]
+    assert pos[0] < 2 <= pos[-1]  # reference images in both sub-batch graphs
+    y64 = y64_all[[meta["ref_images"].index(idx[k]) for k in pos]]
+    conf, iou = meta["conf"], meta["iou"]
+    x = blob_images(meta["batch_full"], 640, seed=meta["seed"])[idx].cuda()
     refs = {}
     for streams in (1, 2):  # the plain session of the same layout (one bs4 graph / two bs2 graphs)
-        plain = p.session(4, 640, 640, half=True, conf=0.25, iou=0.7, streams=streams)
+        plain = p.session(4, 640, 640, half=True, conf=conf, iou=iou, streams=streams)
         refs[streams] = tuple(t.clone() for t in plain(x))
+    o16 = meta["oracle_fp16"]
+    tb, tc = fp16_rule(o16)
+    ref_dets = detections(y64, conf, iou, (640, 640))
     store = dist.FileStore(str(tmp_path / "store"), 1)
     dist.init_process_group("nccl", rank=0, world_size=1, store=store)
     try:
         for streams in (1, 2):
-            sp = ShardedPredictor(p, 4, 640, 640, torch.device("cuda", 0), half=True, conf=0.25, iou=0.7,
-                                  streams=streams)
+            sp = ShardedPredictor(p, 4, 640, 640, torch.device("cuda", 0), half=True, conf=conf, iou=iou,
+                                  streams=streams, keep_pred=True)
             det, cnt = sp(images_global=x)
             torch.cuda.synchronize()
             det_ref, cnt_ref = refs[streams]
@@ -380,5 +419,14 @@ def test_sharded_predictor_nccl_world1(golden_dir, tmp_path):
             assert torch.equal(cnt.cpu(), cnt_ref.cpu()) and int(cnt.sum()) > 0
             assert torch.equal(det.cpu(), det_ref.cpu())
             assert det.data_ptr() == sp.gathered.data_ptr()  # views of the gathered buffer, no copy
+            # against the oracle: decoded predictions and the gathered final detections on the reference images
+            st = err_stats(sp.session.pred.cpu()[pos], y64)
+            for k in ("box_max", "box_p999", "conf_max", "conf_p999"):
+                assert st[k] <= 2 * o16[k] + (1e-2 if k.startswith("box") else 1e-4), (k, st, o16)
+            got = [det[k, : int(cnt[k])].cpu() for k in pos]
+            m = match_detections(ref_dets, got, y64, conf, iou, tb, tc)
+            print(f"sharded nccl world 1, streams {streams}: images {[idx[k] for k in pos]} at {pos}: {m['pairs']} "
+                  f"pairs, {m['borderline']} borderline, {len(m['mismatches'])} mismatches vs the oracle's fp64")
+            assert m["pairs"] > 0 and len(m["mismatches"]) <= 2 * o16["det_mismatches"] + 2, m["mismatches"][:5]
     finally:
         dist.destroy_process_group()

@@ -12,7 +12,6 @@ execution path (``device='cpu'`` raises).
 
 from __future__ import annotations
 
-import os
 import time
 from collections import OrderedDict
 from pathlib import Path
@@ -20,12 +19,14 @@ from pathlib import Path
 import numpy as np
 import torch
 
-from ..nn.tasks import DetectionModel
+from ..nn.tasks import DetectionModel, weights_signature, ydbl_env
 from .results import Results
-from .session import DetectSession
+from .session import DetectSession, default_streams
 
 DEFAULTS = {"conf": 0.25, "iou": 0.7, "max_det": 300, "half": False, "fp8": False, "device": None, "agnostic_nms": False,
-            "classes": None, "batch": 1, "verbose": False, "imgsz": 640}
+            "classes": None, "batch": 1, "verbose": False, "imgsz": 640,
+            # sub-batch graphs per session (DetectSession): None = default_streams(batch), the benched layout
+            "streams": None}
 
 
 def select_device(device=None) -> torch.device:
@@ -156,7 +157,10 @@ class Model:
                 multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True,
                 streams=1, gather_rows=None, nms=True) -> DetectSession:
         """A compiled (batch, h, w, dtype, NMS settings) inference session; streams > 1 splits the batch into
-        that many concurrently replayed sub-batch graphs (DetectSession)."""
+        that many concurrently replayed sub-batch graphs (DetectSession); streams=None: default_streams(batch),
+        the layout predict() runs and bench.py times."""
+        if streams is None:
+            streams = default_streams(batch)
         dev = select_device(device)
         dtype = torch.float16 if (half or fp8) else torch.float32
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
@@ -165,7 +169,7 @@ class Model:
                # the remaining YDBL_* switches (plan-builder fusions in ydbl.nn.modules; YDBL_DS_LEAN / YDBL_NMS_*
                # in the C-ABI) are read at plan build or at each launch, so a captured graph keeps the routing of
                # its capture: a different switch setting is a different session
-               tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("YDBL_"))))
+               ydbl_env())
         s = self._sessions.get(key)
         if s is None:
             while len(self._sessions) >= self.MAX_SESSIONS:
@@ -174,10 +178,27 @@ class Model:
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
                                   keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip,
                                   streams=streams, gather_rows=gather_rows, nms=nms)
+            s.wsig = weights_signature(self.model)  # the weights its plans folded (see _stale)
             self._sessions[key] = s
         else:
             self._sessions.move_to_end(key)
         return s
+
+    def reset_sessions(self):
+        """Drop every compiled session (after editing weights through ``.data``, which no signature sees)."""
+        self._sessions.clear()
+        self.model.invalidate()
+        return self
+
+    def _stale(self, s) -> bool:
+        """True (and `s` dropped from the cache) when the weights changed since `s` folded them (in-place edits,
+        replaced tensors: nn.tasks.weights_signature).  Called right after a launch, so the ~90 us check runs
+        while the graph does."""
+        if weights_signature(self.model) == s.wsig:
+            return False
+        for k in [k for k, v in self._sessions.items() if v is s]:
+            del self._sessions[k]
+        return True
 
     def predict(self, source=None, stream=False, **kwargs):
         """U/engine/model.py:501-560 + DetectionPredictor.postprocess (U/models/yolo/detect/predict.py:23-41).
@@ -211,9 +232,14 @@ class Model:
         im = im.to(dev, non_blocking=True).float()
         b, _, h, w = im.shape
         s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
-                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"])
+                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
+                         streams=args["streams"])
         t1 = time.perf_counter()
         det, cnt = s(im)
+        if self._stale(s):  # weights edited since the session was compiled: rebuild and run again
+            det, cnt = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"],
+                                    max_det=args["max_det"], agnostic=args["agnostic_nms"], classes=args["classes"],
+                                    device=dev, fp8=args["fp8"], streams=args["streams"])(im)
         counts = cnt.tolist()  # one sync per batch
         t2 = time.perf_counter()
         speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b, "postprocess": 0.0}
@@ -233,9 +259,13 @@ class Model:
         # the reference's NMS does not clip: boxes are clipped to the frame by scale_boxes
         s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
                          agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
-                         clip=False)
+                         clip=False, streams=args["streams"])
         t1 = time.perf_counter()
         det, cnt = s(im)
+        if self._stale(s):
+            det, cnt = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"],
+                                    max_det=args["max_det"], agnostic=args["agnostic_nms"], classes=args["classes"],
+                                    device=dev, fp8=args["fp8"], clip=False, streams=args["streams"])(im)
         counts = cnt.tolist()
         t2 = time.perf_counter()
         results = []

@@ -18,6 +18,16 @@ from .._lib import DecodeDesc, NmsDesc, View
 from ..runtime import BranchGraphRunner, GraphRunner, Plan
 
 
+SPLIT_MIN_BATCH = 4  # the benched layouts: DBL-n bs32 / DBL-s bs8, bs64 / DBL-l 1280 bs8 (bench.py --streams 2)
+
+
+def default_streams(batch: int) -> int:
+    """Sub-batch graphs of the session predict() / DetectionModel.forward build for a batch: 2 from batch 4 up -- the
+    layout bench.py times (DESIGN.md §5: DBL-n bs32 +3 %, DBL-s bs64 +9 %, DBL-l 1280 bs8 +8.5 % over one graph;
+    3-4 branches measured slower) -- else 1 (a bs1 branch per image leaves most of the chip idle)."""
+    return 2 if batch >= SPLIT_MIN_BATCH else 1
+
+
 class DetectSession:
     """streams = k > 1: the batch is split into k contiguous sub-batches, each compiled into its own launch
     plan (own buffers) writing into slices of the shared det / count (/ pred) outputs; the k plans are captured
@@ -226,6 +236,9 @@ class DetectSession:
         return [det[i, : cnt[i]].clone() for i in range(self.batch)]
 
     def feats(self):
+        """Per-level head maps [B, 64+nc, H_i, W_i]: NCHW views of the plan's level buffers (no copy); a split
+        session concatenates its sub-batch plans' maps (a copy)."""
         if self.children:
-            raise RuntimeError("feats() of a split (streams > 1) session: use streams=1")
+            per = [c.compiled.feats() for c in self.children]
+            return [torch.cat([f[i] for f in per]) for i in range(len(per[0]))]
         return self.compiled.feats()

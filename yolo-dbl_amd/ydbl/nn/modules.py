@@ -2,10 +2,17 @@
 
 Each class keeps the reference's constructor signature, submodule names and
 parameter shapes (so ``parse_model`` resolves the DBL YAMLs by class name and
-reference ``state_dict`` keys load unchanged), but instead of a torch
-``forward`` it ``emit``s HIP launches into a ``Plan``:
+reference ``state_dict`` keys load unchanged).  Its compute is ``emit``: HIP
+launches appended to a ``Plan``:
 
     y = module.emit(plan, x, out=None)   # x, y: NHWC TV views (lists for multi-input)
+
+and its ``forward(x)`` (the reference's module contract, ``m(x)`` on a tensor or a
+list of tensors, U/nn/tasks.py:158-161) compiles that emit into a one-module plan
+for x's shapes / dtype / device, caches it, and runs it (``run_module``).  A
+registered plugin class WITHOUT ``emit`` -- a plain torch ``forward`` -- runs
+inside the model's plan as a captured torch step on NCHW views of its input
+(``emit_torch``).
 
 ``out`` (optional) is a destination view, typically a channel slice of a
 concat buffer, so Concat / chunk / C2f / C3 concatenations cost no copies.
@@ -16,16 +23,16 @@ U/nn/tasks.py:217) is folded into its pointwise conv here.
 
 from __future__ import annotations
 
-import os
-
+import ctypes as C
 import math
+import os
 
 import torch
 import torch.nn as nn
 
 from .. import _lib
 from .._lib import ConvDesc, DwConvDesc, HgDesc, View
-from ..runtime import TV, Plan, round_up
+from ..runtime import TV, Plan, Step, round_up, weights_signature, ydbl_env
 
 
 # =============================================================================== weight prep + launches
@@ -314,7 +321,7 @@ def mergeable(convs) -> bool:
 def emit_seq(plan: Plan, mods, x, out=None):
     mods = list(mods)
     for i, m in enumerate(mods):
-        x = m.emit(plan, x, out if i == len(mods) - 1 else None)
+        x = emit_module(m, plan, x, out if i == len(mods) - 1 else None)
     return x
 
 
@@ -322,8 +329,133 @@ def emit_copy(plan: Plan, src: TV, dst: TV):
     plan.launch("ydbl_pool_up_concat", None, src.struct(), None, dst.struct(), what="copy")
 
 
+# =============================================================================== module-level forward(x)
+def _check_input(t, dev=None, dt=None):
+    if not isinstance(t, torch.Tensor) or t.ndim != 4:
+        raise TypeError(f"expected BCHW tensors, got {type(t).__name__} {getattr(t, 'shape', '')}")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"ydbl runs on MI355X (gfx950) only: input on {t.device}, move it to a cuda device")
+    if t.dtype not in (torch.float32, torch.float16):
+        raise TypeError(f"input dtype {t.dtype}: float32 or float16 (half) expected")
+    if (dev is not None and t.device != dev) or (dt is not None and t.dtype != dt):
+        raise ValueError("all inputs of one module call must share device and dtype")
+
+
+class _ModulePlan:
+    """One compiled forward of one module for one input signature: input views the call copies into, the plan,
+    and the function that turns the plan's outputs into fresh NCHW tensors."""
+
+    def __init__(self, m, xs, multi):
+        dev, dt = xs[0].device, xs[0].dtype
+        self.plan = Plan(dev, dt)
+        self.views = [self.plan.alloc(t.shape[0], t.shape[2], t.shape[3], t.shape[1]) for t in xs]
+        inp = self.views if multi else self.views[0]
+        self.finish = m._forward_plan(self.plan, inp) if hasattr(m, "_forward_plan") else _tensor_out(
+            emit_module(m, self.plan, inp))
+        self.wsig = weights_signature(m)
+
+    def __call__(self, xs):
+        with torch.no_grad():
+            for v, t in zip(self.views, xs):
+                v.torch().copy_(t.permute(0, 2, 3, 1))  # NCHW -> the plan's NHWC input buffer
+        self.plan.run()
+        return self.finish()
+
+
+def _tensor_out(y):
+    if isinstance(y, (list, tuple)):
+        return lambda: [v.nchw().contiguous() for v in y]
+    return lambda: y.nchw().contiguous()
+
+
+def run_module(m: nn.Module, x):
+    """forward(x) of a built-in module: x a BCHW cuda tensor (or a list for Concat / FullPAD_Tunnel / HyperACE /
+    FuseModule / Detect) in fp32 or fp16 (the half path); returns fresh NCHW tensors of x's dtype.  The module's
+    emit is compiled once per (input shapes, dtype, device, YDBL_* switches) into a plan with its own buffers (the
+    two most recent kept) and rebuilt when the module's weights change (runtime.weights_signature, checked after
+    the launch).  BN is folded: inference semantics, as the reference after fuse()."""
+    multi = isinstance(x, (list, tuple))
+    xs = list(x) if multi else [x]
+    if not xs:
+        raise ValueError("no inputs")
+    for t in xs:
+        _check_input(t, xs[0].device, xs[0].dtype)
+    key = (tuple(tuple(t.shape) for t in xs), multi, xs[0].dtype, str(xs[0].device), ydbl_env())
+    cache = m.__dict__.setdefault("_fwd_plans", {})
+    mp = cache.pop(key, None)
+    if mp is None:
+        while len(cache) >= 2:
+            cache.pop(next(iter(cache)))
+        with torch.cuda.device(xs[0].device):
+            mp = _ModulePlan(m, xs, multi)
+    cache[key] = mp
+    y = mp(xs)
+    if weights_signature(m) != mp.wsig:  # weights edited since the plan folded them: rebuild, run again
+        with torch.cuda.device(xs[0].device):
+            mp = cache[key] = _ModulePlan(m, xs, multi)
+        y = mp(xs)
+    return y
+
+
+class PlanModule(nn.Module):
+    """Base of the built-in modules: ``forward(x)`` = run_module (the reference's ``m(x)`` contract)."""
+
+    def forward(self, x):
+        return run_module(self, x)
+
+
+def _meta_copy(m: nn.Module) -> nn.Module:
+    import copy
+
+    return copy.deepcopy(m).to("meta")
+
+
+def torch_out_shape(m: nn.Module, src) -> tuple:
+    """NHWC shape of a forward-only plugin's output, from a shape-only (meta) run of its forward on NCHW inputs
+    of the given NHWC shapes."""
+    multi = isinstance(src, list)
+    metas = [torch.empty((s[0], s[3], s[1], s[2]), device="meta") for s in (src if multi else [src])]
+    with torch.no_grad():
+        y = _meta_copy(m)(metas if multi else metas[0])
+    if not isinstance(y, torch.Tensor) or y.ndim != 4:
+        raise TypeError(f"plugin {type(m).__name__}: forward must return one BCHW tensor")
+    return (y.shape[0], y.shape[2], y.shape[3], y.shape[1])
+
+
+def emit_torch(m: nn.Module, plan: Plan, x, out: TV | None = None) -> TV:
+    """A registered plugin module that has only a torch ``forward`` (the reference's plugin contract: any class
+    with forward(x), looked up by name, U/nn/tasks.py:974, called as m(x), :158-161) as one plan step: a device
+    copy of the module in the plan's dtype (weights frozen at build, like every other layer) runs on NCHW views
+    of its NHWC input slices, on the stream the plan runs on -- so it is captured into the step's hipGraph with
+    the HIP launches around it -- and its result is copied into the output view.  The module's forward must be
+    graph-capturable (no host syncs) and must launch on the current stream only (single_stream)."""
+    multi = isinstance(x, (list, tuple))
+    xs = list(x) if multi else [x]
+    shape = torch_out_shape(m, [v.shape for v in xs] if multi else xs[0].shape)
+    y = out if out is not None else plan.alloc(*shape)
+    if y.shape != shape:
+        raise ValueError(f"plugin {type(m).__name__}: output {shape} does not fit the destination {y.shape}")
+    import copy
+
+    dm = copy.deepcopy(m).to(plan.device)
+    if plan.device.type != "meta":
+        dm = dm.to(plan.dtype)
+    dm.eval()
+
+    def step(stream):
+        with torch.cuda.stream(torch.cuda.ExternalStream(stream.value, device=plan.device)), torch.no_grad():
+            ins = [v.nchw() for v in xs]
+            y.nchw().copy_(dm(ins if multi else ins[0]))
+        return 0
+
+    step.single_stream = True
+    step.__name__ = f"torch:{type(m).__name__}"
+    plan.steps.append(Step(step, (), f"torch.{type(m).__name__}", [dm]))
+    return y
+
+
 # =============================================================================== conv.py
-class Conv(nn.Module):
+class Conv(PlanModule):
     """U/nn/modules/conv.py:39-63 — conv -> BN -> SiLU (BN folded at plan time, as fuse() does)."""
 
     default_act = nn.SiLU()
@@ -353,7 +485,7 @@ class DWConv(Conv):
         super().__init__(c1, c2, k, s, g=math.gcd(c1, c2), d=d, act=act)
 
 
-class DSConv(nn.Module):
+class DSConv(PlanModule):
     """U/nn/modules/conv.py:91-108 — dw -> pw -> BN -> SiLU."""
 
     def __init__(self, c_in, c_out, k=3, s=1, p=None, d=1, bias=False):
@@ -373,7 +505,7 @@ class DSConv(nn.Module):
         return emit_conv2d(plan, self.pw, t, out, w, b, _lib.ACT_SILU, res, res_mode, what="DSConv.pw")
 
 
-class GhostConv(nn.Module):
+class GhostConv(PlanModule):
     """U/nn/modules/conv.py:184-197 — cat(y, dw5x5(y)), y = cv1(x)."""
 
     def __init__(self, c1, c2, k=1, s=1, g=1, act=True):
@@ -398,7 +530,7 @@ class GhostConv(nn.Module):
         return y
 
 
-class Concat(nn.Module):
+class Concat(PlanModule):
     """U/nn/modules/conv.py:349-359 — inputs are normally already slices of the output (see tasks.py)."""
 
     def __init__(self, dimension=1):
@@ -468,7 +600,7 @@ def emit_detect_box(plan, seq, x: TV, out: TV) -> bool:
     return True
 
 
-class Bottleneck(nn.Module):
+class Bottleneck(PlanModule):
     """U/nn/modules/block.py:344-357."""
 
     def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
@@ -506,7 +638,7 @@ class Bottleneck(nn.Module):
                              res_mode=_lib.RES_ADD if self.add else _lib.RES_NONE)
 
 
-class C2f(nn.Module):
+class C2f(PlanModule):
     """U/nn/modules/block.py:234-249."""
 
     def __init__(self, c1, c2, n=1, shortcut=False, g=1, e=0.5):
@@ -525,7 +657,7 @@ class C2f(nn.Module):
         return self.cv2.emit(plan, buf, out)
 
 
-class C3(nn.Module):
+class C3(PlanModule):
     """U/nn/modules/block.py:259-273."""
 
     def __init__(self, c1, c2, n=1, shortcut=True, g=1, e=0.5):
@@ -602,7 +734,7 @@ class C3(nn.Module):
                 and c3.in_channels == 2 * c_ and c3.out_channels == c_ and isinstance(self.cv3.act, nn.SiLU))
 
 
-class GhostBottleneck(nn.Module):
+class GhostBottleneck(PlanModule):
     """U/nn/modules/block.py:323-341 (stride 1 on the DBL path)."""
 
     def __init__(self, c1, c2, k=3, s=1):
@@ -633,7 +765,7 @@ class C3Ghost(C3):
         self.m = nn.Sequential(*(GhostBottleneck(c_, c_) for _ in range(n)))
 
 
-class DSBottleneck(nn.Module):
+class DSBottleneck(PlanModule):
     """U/nn/modules/block.py:1408-1444."""
 
     def __init__(self, c1, c2, shortcut=True, e=0.5, k1=3, k2=5, d2=1):
@@ -717,7 +849,7 @@ class AdaHyperedgeGen(nn.Module):
         self.scaling = math.sqrt(self.head_dim)
 
 
-class AdaHGConv(nn.Module):
+class AdaHGConv(PlanModule):
     """U/nn/modules/block.py:1659-1708."""
 
     def __init__(self, embed_dim, num_hyperedges=16, num_heads=4, dropout=0.1, context="both"):
@@ -757,7 +889,7 @@ class AdaHGConv(nn.Module):
         return y
 
 
-class AdaHGComputation(nn.Module):
+class AdaHGComputation(PlanModule):
     """U/nn/modules/block.py:1710-1752 (NHWC pixels are already the token sequence)."""
 
     def __init__(self, embed_dim, num_hyperedges=16, num_heads=8, dropout=0.1, context="both"):
@@ -769,7 +901,7 @@ class AdaHGComputation(nn.Module):
         return self.hgnn.emit(plan, x, out)
 
 
-class C3AH(nn.Module):
+class C3AH(PlanModule):
     """U/nn/modules/block.py:1754-1795."""
 
     def __init__(self, c1, c2, e=1.0, num_hyperedges=8, context="both"):
@@ -795,7 +927,7 @@ class C3AH(nn.Module):
         return self.cv3.emit(plan, buf, out)
 
 
-class FuseModule(nn.Module):
+class FuseModule(PlanModule):
     """U/nn/modules/block.py:1797-1840."""
 
     def __init__(self, c_in, channel_adjust):
@@ -811,7 +943,7 @@ class FuseModule(nn.Module):
         return self.conv_out.emit(plan, cat, out)
 
 
-class HyperACE(nn.Module):
+class HyperACE(PlanModule):
     """U/nn/modules/block.py:1842-1895."""
 
     def __init__(self, c1, c2, n=1, num_hyperedges=8, dsc3k=True, shortcut=False, e1=0.5, e2=1, context="both",
@@ -868,7 +1000,7 @@ class HyperACE(nn.Module):
         emit_conv2d(plan, b1.cv3.conv, bb.cslice(4 * c_, 2 * c_), out1, w, b, _act_code(b1.cv3.act), what="Conv1x1")
 
 
-class DownsampleConv(nn.Module):
+class DownsampleConv(PlanModule):
     """U/nn/modules/block.py:1897-1928."""
 
     def __init__(self, in_channels, channel_adjust=True):
@@ -883,7 +1015,7 @@ class DownsampleConv(nn.Module):
         return self.channel_adjust.emit(plan, pooled, out) if adjust else pooled
 
 
-class FullPAD_Tunnel(nn.Module):  # noqa: N801 (reference name)
+class FullPAD_Tunnel(PlanModule):  # noqa: N801 (reference name)
     """U/nn/modules/block.py:1930-1956 — x0 + gate * x1."""
 
     def __init__(self):
@@ -913,7 +1045,7 @@ class FullPAD_Tunnel(nn.Module):  # noqa: N801 (reference name)
 
 
 # =============================================================================== DySample / LSKblock
-class DySample(nn.Module):
+class DySample(PlanModule):
     """U/nn/modules_upsample/DySample.py:20-81 (style 'lp', scale 2, groups 4, no scope)."""
 
     def __init__(self, in_channels, scale=2, style="lp", groups=4, dyscope=False):
@@ -956,7 +1088,7 @@ class DySample(nn.Module):
         return y
 
 
-class LSKblock(nn.Module):
+class LSKblock(PlanModule):
     """U/nn/modules_attention/LSKA.py:28-52."""
 
     def __init__(self, dim):
@@ -1014,7 +1146,7 @@ class DFL(nn.Module):
         self.c1 = c1
 
 
-class Detect(nn.Module):
+class Detect(PlanModule):
     """U/nn/modules/head.py:21-198 — per level cat(cv2 box branch, cv3 cls branch); decode in ydbl_detect_decode."""
 
     dynamic = False
@@ -1057,6 +1189,31 @@ class Detect(nn.Module):
             a[-1].bias.data[:] = 1.0
             b[-1].bias.data[: self.nc] = math.log(5 / self.nc / (640 / s) ** 2)
 
+    def _forward_plan(self, plan, xs):
+        """forward(x) in inference mode (head.py:108-118 with export False): the per-level maps x[i] =
+        cat(box, cls) and y = _inference(x) (head.py:143-181: DFL, make_anchors, dist2bbox, sigmoid) decoded by
+        ydbl_detect_decode into y [B, 4+nc, A] (no candidates: the threshold is above every score).  Returns the
+        call's finisher -> (y, [x_i]) as fresh tensors of the plan's dtype."""
+        if not float(self.stride.abs().sum()):
+            raise RuntimeError("Detect.stride is unset: build the module through DetectionModel (stride probe)")
+        levels = self.emit(plan, xs)
+        B = levels[0].n
+        A = sum(lv.h * lv.w for lv in levels)
+        dev = plan.device
+        pred = torch.empty((B, 4 + self.nc, A), dtype=torch.float32, device=dev)
+        cand = [torch.empty((B, A, 4), dtype=torch.float32, device=dev), torch.empty((B, A), dtype=torch.float32,
+                device=dev), torch.empty((B, A), dtype=torch.int32, device=dev),
+                torch.empty((B, A), dtype=torch.int32, device=dev), torch.zeros((B,), dtype=torch.int32, device=dev)]
+        plan.buffers += [pred, *cand]
+        boxes = (View * 3)(*[lv.cslice(0, 4 * self.reg_max).struct() for lv in levels])
+        clss = (View * 3)(*[lv.cslice(4 * self.reg_max, self.nc).struct() for lv in levels])
+        strides = (C.c_float * 3)(*[float(s) for s in self.stride.tolist()])
+        dd = _lib.DecodeDesc(boxes, clss, len(levels), self.nc, strides, 2.0, 0, None, 0, pred.data_ptr(),
+                             *[t.data_ptr() for t in cand], A)
+        plan.launch("ydbl_detect_decode", dd, what="Detect.decode", keep=[dd])
+        dt = plan.dtype
+        return lambda: (pred.to(dt, copy=True), [lv.nchw().contiguous() for lv in levels])
+
     def emit(self, plan, xs, out=None):
         """Per level: one NHWC buffer [B,h,w,64+nc] (box logits | class logits) = the reference's x[i]."""
         levels = []
@@ -1083,9 +1240,12 @@ class Detect(nn.Module):
 
 
 def emit_module(m: nn.Module, plan: Plan, x, out=None):
-    """Emit any parsed layer: plugin modules or nn.Sequential repeats."""
+    """Emit any parsed layer: built-in modules (HIP launches), nn.Sequential repeats, and registered plugin
+    classes that only have a torch forward (emit_torch)."""
     if isinstance(m, nn.Sequential):
         return emit_seq(plan, m, x, out)
-    if not hasattr(m, "emit"):
-        raise NotImplementedError(f"{type(m).__name__} has no HIP implementation")
-    return m.emit(plan, x, out)
+    if hasattr(m, "emit"):
+        return m.emit(plan, x, out)
+    if type(m).forward is not nn.Module.forward:
+        return emit_torch(m, plan, x, out)
+    raise NotImplementedError(f"{type(m).__name__} has neither emit() nor forward()")

@@ -23,7 +23,7 @@ from pathlib import Path
 import torch
 import torch.nn as nn
 
-from ..runtime import TV, Plan, round_up
+from ..runtime import TV, Plan, round_up, weights_signature, ydbl_env  # noqa: F401 (re-exported)
 from . import modules as M
 
 CFG_DIR = Path(__file__).resolve().parent.parent / "cfg" / "models"
@@ -42,7 +42,11 @@ _C1_ONLY = {"DySample", "LSKblock"}
 
 
 def register_module(cls, name: str | None = None):
-    """Plug a module class in under a YAML name (same constructor contract as the reference)."""
+    """Plug a module class in under a YAML name (same constructor contract as the reference, whose parse_model
+    resolves names through globals(), U/nn/tasks.py:974).  Either contract works: a class with
+    ``emit(plan, x, out)`` (HIP launches, as the built-ins) or a plain torch ``forward(x)``, which runs inside the
+    compiled plan as a captured torch step on NCHW views of its inputs (nn.modules.emit_torch).  Channel
+    bookkeeping for a plugin name follows the reference's rule for names it does not know (c2 = ch[f])."""
     REGISTRY[name or cls.__name__] = cls
     return cls
 
@@ -217,28 +221,42 @@ class DetectionModel(nn.Module):
         b, _, h, w = x.shape
         s = self._forward_session(b, h, w, x.dtype == torch.float16, x.device)
         s(x.float())
+        sig = weights_signature(self)  # checked while the graph runs
+        if sig != s.wsig:  # weights edited since the plan was compiled: rebuild, run again
+            s = self._forward_session(b, h, w, x.dtype == torch.float16, x.device, fresh=sig)
+            s(x.float())
         y = s.pred.to(x.dtype, copy=True)
         feats = [f.contiguous() for f in s.feats()]
         return y, feats
 
-    def _forward_session(self, b, h, w, half, device):
-        from ..engine.session import DetectSession
+    def _forward_session(self, b, h, w, half, device, fresh=None):
+        from ..engine.session import DetectSession, default_streams
 
         cache = self.__dict__.setdefault("_fwd_sessions", {})
-        key = (b, h, w, half, str(device))
+        # compiled plans hold the routing of the YDBL_* switches at build time (part of the key) and BN-folded
+        # copies of the weights (the session's wsig, checked by forward() after each launch)
+        key = (b, h, w, half, str(device), ydbl_env())
         s = cache.pop(key, None)
+        if s is not None and fresh is not None and s.wsig != fresh:
+            s = None  # weights changed since this plan was built
         if s is None:
             while len(cache) >= self.MAX_FORWARD_SESSIONS:
                 cache.pop(next(iter(cache)))
             with torch.cuda.device(device):
                 s = DetectSession(self, b, h, w, torch.float16 if half else torch.float32, keep_pred=True, nms=False,
-                                  device=device)
+                                  device=device, streams=default_streams(b))
+            s.wsig = weights_signature(self)
         cache[key] = s  # most recently used last
         return s
 
+    def invalidate(self):
+        """Drop every compiled forward plan (after editing weights through ``.data``)."""
+        self.__dict__.pop("_fwd_sessions", None)
+        return self
+
     def load_state_dict(self, *args, **kwargs):
         """nn.Module.load_state_dict; compiled forward plans hold folded copies of the weights, so they go."""
-        self.__dict__.pop("_fwd_sessions", None)
+        self.invalidate()
         return super().load_state_dict(*args, **kwargs)
 
     def fuse(self, verbose=False):
@@ -356,7 +374,9 @@ def _propagate_shapes(layers, batch, h, w, ch):
             cur = (batch, src[0][1], src[0][2], sum(s_[3] for s_ in src))
         elif t == "Detect":
             cur = None
+        elif not hasattr(mm, "emit"):  # a registered forward-only plugin: its output shape from a meta run
+            cur = M.torch_out_shape(m, src)
         else:
-            raise NotImplementedError(t)
+            raise NotImplementedError(f"{t}: a registered module with emit() needs a shape rule here")
         shapes.append(cur)
     return shapes

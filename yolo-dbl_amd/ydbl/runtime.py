@@ -11,6 +11,8 @@ replays it, so the per-forward host cost is a single graph launch.
 from __future__ import annotations
 
 import ctypes as C
+import operator
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -18,6 +20,40 @@ import torch
 
 from . import _lib
 from ._lib import View, lib
+
+
+def ydbl_env() -> tuple:
+    """The YDBL_* switches (plan-builder fusions, C-ABI routing), read when a plan is built or launched: part of
+    every compiled-plan cache key."""
+    return tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("YDBL_")))
+
+
+_STRUCT_EPOCH = [0]  # bumped whenever any module registers a parameter, buffer or submodule (torch global hooks)
+
+
+def _bump_epoch(*_):
+    _STRUCT_EPOCH[0] += 1
+
+
+for _reg in ("register_module_parameter_registration_hook", "register_module_buffer_registration_hook",
+             "register_module_module_registration_hook"):
+    getattr(torch.nn.modules.module, _reg)(_bump_epoch)
+_VERSION = operator.attrgetter("_version")
+
+
+def weights_signature(module: torch.nn.Module) -> tuple:
+    """Identity + summed version counters of the module's floating-point parameters and buffers.  A compiled plan
+    holds BN-folded copies of the weights taken at build time; the signature changes when a tensor is replaced
+    (a registration, caught by the global hooks above) or edited in place through a tracked op (p.copy_() under
+    no_grad, load_state_dict, optimizer steps).  Edits through ``.data`` bypass the version counter: call
+    ``invalidate()`` / ``Model.reset_sessions()`` after those.  ~90 us for DBL-n's 607 tensors: callers check it
+    while the graph runs (Model.predict, DetectionModel.forward)."""
+    c = module.__dict__.get("_wsig_cache")
+    if c is None or c[0] != _STRUCT_EPOCH[0]:
+        ts = [t for t in (*module.parameters(), *module.buffers()) if t.is_floating_point()]
+        c = (_STRUCT_EPOCH[0], ts, hash(tuple((id(t), t.data_ptr()) for t in ts)))
+        module.__dict__["_wsig_cache"] = c
+    return c[2], sum(map(_VERSION, c[1]))
 
 
 def round_up(x: int, m: int) -> int:
@@ -148,6 +184,16 @@ class Plan:
         self.steps[writer[0]].keep.append((y2, r2))
         return y2
 
+    def check_single_stream(self):
+        """Every step must run on the one stream it is handed: a libydbl C-ABI entry point (they launch on their
+        stream argument only) or a step flagged ``single_stream``.  BranchGraphRunner captures plans as forked
+        branches, and on this ROCm a stream fork from inside a forked branch segfaults hipStreamEndCapture
+        (the head-branch experiment), so a step that forks streams must never reach a branch."""
+        for st in self.steps:
+            if not (isinstance(st.fn, C._CFuncPtr) or getattr(st.fn, "single_stream", False)):
+                raise RuntimeError(f"plan step '{st.what}' ({st.fn!r}) is not a single-stream launch: it cannot be "
+                                   f"captured as a branch of a split session's graph")
+
     def run(self, stream: int | None = None):
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream if stream is None else stream)
         for st in self.steps:
@@ -234,6 +280,8 @@ class BranchGraphRunner:
     (scripts/graph_branch_probe.py)."""
 
     def __init__(self, plans, warmup: int = 1):
+        for p in plans:
+            p.check_single_stream()
         dev = plans[0].device
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
