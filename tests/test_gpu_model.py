@@ -430,3 +430,37 @@ def test_sharded_predictor_nccl_world1(golden_dir, tmp_path):
             assert m["pairs"] > 0 and len(m["mismatches"]) <= 2 * o16["det_mismatches"] + 2, m["mismatches"][:5]
     finally:
         dist.destroy_process_group()
+
+
+def test_fp8_calibration_reads_inputs_at_launch(golden_dir):
+    """ydbl.quant.calibrate takes each conv's statistics right before its launch: HyperACE's merged branch 1x1
+    (C3AHx2.cv1|cv2) reads y1, whose slice branch1.cv3 overwrites later in the plan, so the scale and the bias
+    correction must come from y1 as that conv reads it, not from the buffer after the plan ran."""
+    from ydbl import quant
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    s = p.session(2, 256, 256, half=True, keep_pred=True, use_graph=False)
+    s.load(blob_images(2, 256, seed=4321).cuda())
+    plan = s.plan
+    keys = quant.candidate_keys(plan)
+    steps = quant._candidate_steps(plan)
+    k_step, ci = next((k, c) for k, c in steps.items() if plan.steps[k].what == "C3AHx2.cv1|cv2")
+    got = {}
+
+    def grab(k):
+        if k == k_step:
+            got["x"] = plan.fp8_candidates[ci][1].torch().float().clone()
+
+    plan.run_observed(grab)
+    torch.cuda.synchronize()
+    x_at_launch = got["x"]
+    x_after = plan.fp8_candidates[ci][1].torch().float()
+    assert not torch.equal(x_at_launch, x_after)  # the hazard is real: the buffer is rewritten after the launch
+    cal = quant.calibrate([plan], plan.run, rank=False)
+    qs = quant.E4M3_MAX / x_at_launch.abs().amax().item()
+    assert abs(cal.qs[keys[ci]] - qs) <= 1e-6 * qs
+    d0, _, w32 = plan.fp8_candidates[ci]
+    wq, sw = quant.quantize_weights_e4m3(w32)
+    ref = quant.bias_delta([x_at_launch], cal.qs[keys[ci]], w32, wq, sw, d0.kh * d0.kw)
+    assert torch.allclose(torch.tensor(cal.delta[keys[ci]]), ref, rtol=1e-4, atol=1e-6)

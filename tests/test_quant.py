@@ -38,3 +38,36 @@ def test_selected_fraction_with_a_stride2_candidate():
     assert chosen == [0, 1, 2] and frac == 1.0
     chosen, frac = select_by_mac_budget([0.1, 0.9, 0.2], macs, 0.0)
     assert chosen == [] and frac == 0.0
+
+
+def test_candidate_keys_stable_across_layouts():
+    """ydbl.quant.candidate_keys names a model's fp8 candidates the same way at every batch / sub-batch size, so one
+    committed calibration (tests/golden/fp8_calib_*.json) means one layer set for every layout the model runs."""
+    from ydbl import YOLO
+    from ydbl.quant import candidate_keys
+
+    m = YOLO("yolov13s_DBL.yaml", nc=3).model
+    keys = {}
+    for b in (1, 4, 16, 32):
+        plan = m.compile(b, 640, 640, torch.float16, device="meta").plan
+        k = candidate_keys(plan)
+        assert len(k) == len(set(k)) == len(plan.fp8_candidates) > 0
+        assert all(int(key[1:].split(".")[0]) >= 0 for key in k)  # every candidate knows its layer
+        keys[b] = k
+    assert keys[16] == keys[32]
+    # small maps fold DSC3k's 128-channel cv3 into the lean DSConv launch (no longer a candidate): the others keep
+    # their names
+    assert set(keys[1]) == set(keys[4]) < set(keys[32])
+
+
+def test_calibration_roundtrip_and_shares(tmp_path):
+    from ydbl.quant import Fp8Calibration
+
+    cal = Fp8Calibration({"a": 1.0, "b": 2.0, "c": 3.0}, {"a": [0.0], "b": [0.1], "c": [0.2]},
+                         sens={"a": 0.3, "b": 0.1, "c": 0.2}, macs={"a": 10, "b": 60, "c": 30}, meta={"x": 1})
+    path = cal.save(tmp_path / "cal.json")
+    back = Fp8Calibration.load(path)
+    assert back.to_json() == cal.to_json()
+    assert back.switched(1.0) == ["a", "b", "c"]
+    assert back.switched(0.3) == ["c"]  # b (least sensitive) is 60 % of the MACs: skipped, c fits
+    assert back.switched(0.95) == ["b", "c"] and abs(back.mac_fraction(["b", "c"]) - 0.9) < 1e-12

@@ -26,7 +26,9 @@ from .session import DetectSession, default_streams
 DEFAULTS = {"conf": 0.25, "iou": 0.7, "max_det": 300, "half": False, "fp8": False, "device": None, "agnostic_nms": False,
             "classes": None, "batch": 1, "verbose": False, "imgsz": 640,
             # sub-batch graphs per session (DetectSession): None = default_streams(batch), the benched layout
-            "streams": None}
+            "streams": None,
+            # fp8: an ydbl.quant.Fp8Calibration or its JSON file (None: calibrate on the first batch)
+            "fp8_calibration": None}
 
 
 def select_device(device=None) -> torch.device:
@@ -51,6 +53,14 @@ def select_device(device=None) -> torch.device:
 
 def load_tensor_source(im: torch.Tensor, stride: int = 32) -> torch.Tensor:
     """LoadTensor._single_check (U/data/loaders.py:515-580): BCHW, H and W divisible by the stride, /255 if >1."""
+    im = check_tensor_source(im, stride)
+    if im.max() > 1.0 + torch.finfo(im.dtype).eps:
+        im = im.float() / 255.0
+    return im
+
+
+def check_tensor_source(im, stride: int = 32) -> torch.Tensor:
+    """The shape rules of LoadTensor._single_check (no device work): a BCHW tensor (or a list of CHW / 1CHW)."""
     if isinstance(im, (list, tuple)):
         im = torch.stack([t if t.ndim == 3 else t[0] for t in im])
     if not isinstance(im, torch.Tensor):
@@ -62,8 +72,6 @@ def load_tensor_source(im: torch.Tensor, stride: int = 32) -> torch.Tensor:
     if im.shape[2] % stride or im.shape[3] % stride:
         raise ValueError(
             f"torch.Tensor inputs should be BCHW with height and width divisible by stride {stride}; got {tuple(im.shape)}")
-    if im.max() > 1.0 + torch.finfo(im.dtype).eps:
-        im = im.float() / 255.0
     return im
 
 
@@ -155,7 +163,7 @@ class Model:
 
     def session(self, batch, h, w, half=False, conf=0.25, iou=0.7, max_det=300, agnostic=False, classes=None,
                 multi_label=False, device=None, keep_pred=False, use_graph=True, fp8=False, clip=True,
-                streams=1, gather_rows=None, nms=True) -> DetectSession:
+                streams=1, gather_rows=None, nms=True, fp8_calibration=None) -> DetectSession:
         """A compiled (batch, h, w, dtype, NMS settings) inference session; streams > 1 splits the batch into
         that many concurrently replayed sub-batch graphs (DetectSession); streams=None: default_streams(batch),
         the layout predict() runs and bench.py times."""
@@ -166,6 +174,7 @@ class Model:
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
                float(fp8), bool(clip), int(streams), gather_rows, bool(nms),
+               str(fp8_calibration) if isinstance(fp8_calibration, (str, Path)) else id(fp8_calibration),
                # the remaining YDBL_* switches (plan-builder fusions in ydbl.nn.modules; YDBL_DS_LEAN / YDBL_NMS_*
                # in the C-ABI) are read at plan build or at each launch, so a captured graph keeps the routing of
                # its capture: a different switch setting is a different session
@@ -177,7 +186,7 @@ class Model:
             with torch.cuda.device(dev):
                 s = DetectSession(self.model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes,
                                   keep_pred=keep_pred, use_graph=use_graph, device=dev, fp8=fp8, clip=clip,
-                                  streams=streams, gather_rows=gather_rows, nms=nms)
+                                  streams=streams, gather_rows=gather_rows, nms=nms, fp8_calibration=fp8_calibration)
             s.wsig = weights_signature(self.model)  # the weights its plans folded (see _stale)
             self._sessions[key] = s
         else:
@@ -228,23 +237,34 @@ class Model:
                 paths, frames = frames_from_images(source)
                 return self._predict_frames(frames, args, dev, t0, stream, paths)
             raise TypeError(f"unsupported source type {type(source).__name__}")
-        im = load_tensor_source(source, int(self.model.stride.max()))
-        im = im.to(dev, non_blocking=True).float()
+        im = check_tensor_source(source, int(self.model.stride.max()))
+        big = None
+        if im.device == dev:  # LoadTensor's /255 rule, on the tensor's device: the reduction runs during the lookup
+            big = im.amax() > 1.0 + (torch.finfo(im.dtype).eps if im.is_floating_point() else 0.0)
+        else:  # host tensors are scaled on the host, where the reference's LoadTensor does it, then moved
+            im = load_tensor_source(im).to(dev, non_blocking=True)
         b, _, h, w = im.shape
         s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
                          agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
-                         streams=args["streams"])
+                         streams=args["streams"], fp8_calibration=args["fp8_calibration"])
+        im = im.float() / 255.0 if big is not None and bool(big) else im.float()
         t1 = time.perf_counter()
         det, cnt = s(im)
         if self._stale(s):  # weights edited since the session was compiled: rebuild and run again
             det, cnt = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"],
                                     max_det=args["max_det"], agnostic=args["agnostic_nms"], classes=args["classes"],
-                                    device=dev, fp8=args["fp8"], streams=args["streams"])(im)
+                                    device=dev, fp8=args["fp8"], streams=args["streams"],
+                                    fp8_calibration=args["fp8_calibration"])(im)
         counts = cnt.tolist()  # one sync per batch
         t2 = time.perf_counter()
         speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b, "postprocess": 0.0}
-        results = [Results(im[i].permute(1, 2, 0), path=f"image{i}.jpg", names=self.model.names,
-                           boxes=det[i, : counts[i]].clone(), speed=speed) for i in range(b)]
+        # one copy of the batch's detections (the session's buffers are reused by the next call); each image's
+        # boxes are a view of it, and orig_img a view of the input batch (HWC, as LoadTensor hands it over)
+        dets = det[:, : max(counts, default=0)].clone()
+        hwc = im.permute(0, 2, 3, 1)
+        names = self.model.names
+        results = [Results(hwc[i], path=f"image{i}.jpg", names=names, boxes=dets[i, : counts[i]], speed=speed)
+                   for i in range(b)]
         return iter(results) if stream else results
 
     def _predict_frames(self, frames, args, dev, t0, stream, paths=None):
@@ -259,13 +279,14 @@ class Model:
         # the reference's NMS does not clip: boxes are clipped to the frame by scale_boxes
         s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
                          agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
-                         clip=False, streams=args["streams"])
+                         clip=False, streams=args["streams"], fp8_calibration=args["fp8_calibration"])
         t1 = time.perf_counter()
         det, cnt = s(im)
         if self._stale(s):
             det, cnt = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"],
                                     max_det=args["max_det"], agnostic=args["agnostic_nms"], classes=args["classes"],
-                                    device=dev, fp8=args["fp8"], clip=False, streams=args["streams"])(im)
+                                    device=dev, fp8=args["fp8"], clip=False, streams=args["streams"],
+                                    fp8_calibration=args["fp8_calibration"])(im)
         counts = cnt.tolist()
         t2 = time.perf_counter()
         results = []

@@ -39,11 +39,12 @@ class DetectSession:
     def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
                  multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
                  keep_pred=False, use_graph=True, device="cuda", fp8=False, streams=1, gather_rows=None, nms=True,
-                 _outputs=None):
+                 fp8_calibration=None, _outputs=None):
         if fp8 and dtype != torch.float16:
             raise ValueError("fp8 operands run on the fp16 activation path (half=True)")
         self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
         self.fp8, self.fp8_ready = bool(fp8), False
+        self.fp8_calibration = fp8_calibration  # an Fp8Calibration / its file, applied at the first launch
         # fp8=True: every candidate conv in e4m3; fp8=<float in (0, 1)>: that share of the candidates'
         # MACs, least output-sensitive first (ydbl.quant.enable_fp8)
         self.fp8_fraction = float(fp8) if not isinstance(fp8, bool) and 0 < float(fp8) < 1 else 1.0
@@ -165,14 +166,17 @@ class DetectSession:
             raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
         self.compiled.input.copy_(x, non_blocking=True)
 
-    def calibrate_fp8(self, x: torch.Tensor | None = None, fraction: float | None = None) -> int:
-        """Switch the dense convs to e4m3 operands (ydbl.quant), with activation scales from one fp16
-        pass over `x` (default: the batch already loaded).  fraction < 1: only that share of the
-        candidates' MACs, least output-sensitive convs first (default: the session's fp8_fraction).
-        Returns the number of convs switched."""
-        from ..quant import enable_fp8
+    def calibrate_fp8(self, x: torch.Tensor | None = None, fraction: float | None = None, calibration=None) -> int:
+        """Switch the dense convs to e4m3 operands (ydbl.quant).  calibration (an ydbl.quant.Fp8Calibration or the
+        path of one saved with .save()): its activation scales, bias corrections and layer set; else one measured
+        now on `x` (default: the batch already loaded) -- kept as self.fp8_calibration, .save() it to reuse.
+        fraction < 1: only that share of the candidates' MACs, least output-sensitive convs first (default: the
+        session's fp8_fraction).  Returns the number of convs switched."""
+        from ..quant import Fp8Calibration, enable_fp8
 
-        if x is not None:
+        if isinstance(calibration, (str, bytes)) or hasattr(calibration, "__fspath__"):
+            calibration = Fp8Calibration.load(calibration)
+        if x is not None and calibration is None:
             self.load(x)
         frac = self.fp8_fraction if fraction is None else float(fraction)
         # one joint calibration over every sub-batch plan (ydbl.quant.enable_fp8): the same activation scales
@@ -186,7 +190,8 @@ class DetectSession:
         def heads():
             return [t for c in owners for t in c.compiled.feats()]
 
-        n = enable_fp8([c.plan for c in owners], run_all, fraction=frac, head=heads)
+        n = enable_fp8([c.plan for c in owners], run_all, fraction=frac, head=heads, calibration=calibration)
+        self.fp8_calibration = owners[0].plan.fp8_calibration
         for c in owners:
             c._graph = None  # descriptors changed: recapture
             c.fp8_ready = True
@@ -201,7 +206,8 @@ class DetectSession:
 
     def launch(self):
         if self.fp8 and not self.fp8_ready:
-            self.calibrate_fp8()  # first batch calibrates (dynamic post-training quantization)
+            # a given calibration, else the first batch calibrates (dynamic post-training quantization)
+            self.calibrate_fp8(calibration=self.fp8_calibration)
         if self.children and self.use_graph:  # every sub-batch plan a branch of one graph: one launch
             if self._graph is None:
                 self._graph = BranchGraphRunner(self.plans)

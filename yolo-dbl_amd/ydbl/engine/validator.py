@@ -94,7 +94,8 @@ class DetectionValidator:
         return self.model.session(b, h, w, half=a.get("half", False), conf=a["conf"], iou=a["iou"],
                                   max_det=a.get("max_det", 300), multi_label=True,
                                   agnostic=a.get("agnostic_nms", False) or a.get("single_cls", False), device=dev,
-                                  fp8=a.get("fp8", False), clip=clip, streams=a.get("streams") or 1)
+                                  fp8=a.get("fp8", False), clip=clip, streams=a.get("streams") or 1,
+                                  fp8_calibration=a.get("fp8_calibration"))
 
     def _run_tensor_batch(self, batch, dev):
         im = load_tensor_source(batch["img"], int(self.model.model.stride.max())).to(dev).float()

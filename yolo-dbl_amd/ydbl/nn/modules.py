@@ -102,6 +102,7 @@ def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None
     if plan.dtype == torch.float16 and x.c >= 64 and not what.startswith("Detect."):
         d._b32 = b.detach().float().cpu() if b is not None else None  # (ydbl.quant's bias correction)
         plan.fp8_candidates.append((d, x, wk32))  # see ydbl.quant: e4m3 operands after calibration
+        plan.fp8_layers.append(getattr(plan, "cur_layer", -1))
 
 
 def dw_desc(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None, stride=1, pad=0, dil=1,

@@ -302,6 +302,7 @@ class DetectionModel(nn.Module):
             plan.launch("ydbl_input_nchw_to_nhwc", x_nchw.data_ptr(), batch, self.yaml["ch"], h, w, 1.0, inp.struct(),
                         what="input")
         for m in layers:
+            plan.cur_layer = m.i  # (ydbl.quant names fp8 candidates by the layer that emitted them)
             if stem2 and m is layers[1]:
                 y.append(x)
                 continue

@@ -122,6 +122,7 @@ class Plan:
         self.bytes_allocated = 0
         self._writers: dict = {}  # view key -> (step index, desc) of the conv / DySample launch that wrote it
         self.fp8_candidates: list = []  # (ConvDesc, input view, fp32 [Cout][KPAD] weights) of fp8-able convs
+        self.fp8_layers: list = []  # the model layer index that emitted each candidate (-1 outside a model)
 
     # ---------------------------------------------------------------- memory
     def alloc(self, n: int, h: int, w: int, c: int, dtype: torch.dtype | None = None, cs: int | None = None) -> TV:
@@ -193,6 +194,16 @@ class Plan:
             if not (isinstance(st.fn, C._CFuncPtr) or getattr(st.fn, "single_stream", False)):
                 raise RuntimeError(f"plan step '{st.what}' ({st.fn!r}) is not a single-stream launch: it cannot be "
                                    f"captured as a branch of a split session's graph")
+
+    def run_observed(self, observe, stream: int | None = None):
+        """Plan.run with observe(step_index) called before every step, on the host, in launch order (the observer
+        may enqueue its own device work on the current stream: it sees every buffer exactly as that step will)."""
+        s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream if stream is None else stream)
+        for i, st in enumerate(self.steps):
+            observe(i)
+            rc = st.fn(*st.args, s)
+            if rc:
+                _lib.check(rc, st.what)
 
     def run(self, stream: int | None = None):
         s = C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream if stream is None else stream)
