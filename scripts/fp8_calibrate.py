@@ -8,7 +8,11 @@ sub-batch layout runs it.  Then the config-5 protocol (tests/test_gpu_model.py::
 16 evaluation images, pseudo-GT = the CPU oracle's fp32 detections at conf 0.0171, val at conf 0.001) for each share,
 twice (the drop must repeat exactly).
 
-    python scripts/fp8_calibrate.py [--no-save] [share ...]     (default shares: 0.1 0.25 0.5 1.0)
+    python scripts/fp8_calibrate.py [--no-save] [--head-metric] [share ...]     (default shares: 0.1 0.25 0.5 1.0)
+
+Ranking (default): each candidate conv ALONE in e4m3, its mAP50 drop on the calibration images against the fp16
+path's own detections there (no oracle: product code only); --head-metric: the mean |delta| of the Detect head maps
+(ydbl.quant.calibrate's built-in ranking).
 """
 import sys
 from pathlib import Path
@@ -30,17 +34,39 @@ def main():
     save = "--no-save" not in args
     shares = [float(a) for a in args if not a.startswith("--")] or [0.1, 0.25, 0.5, 1.0]
     p, o = T._models("yolov13s_DBL.yaml", 3, ROOT / "tests" / "golden")
+    task = "--head-metric" not in args
     if save or not CAL.exists():
+        xc = blob_images(32, 640, seed=4321)
         s = p.session(32, 640, 640, half=True, conf=0.25, iou=0.7, keep_pred=True, use_graph=False)
-        s.load(blob_images(32, 640, seed=4321).cuda())
-        cal = quant.calibrate([s.plan], s.plan.run, head=s.compiled.feats, meta={
+        s.load(xc.cuda())
+        cal = quant.calibrate([s.plan], s.plan.run, head=s.compiled.feats, rank=not task, meta={
             "model": "yolov13s_DBL.yaml nc 3", "weights": "tests/golden/trained_yolov13s_DBL_nc3.npz",
             "calibration_images": "ydbl.utils.synthetic.blob_images(32, 640, seed=4321), one bs32 fp16 plan",
-            "sens": "mean |delta| of the Detect head maps with the conv alone in e4m3",
+            "sens": ("mAP50 drop on the calibration images with the conv alone in e4m3, against the fp16 path's own "
+                     "detections (conf .25) as pseudo ground truth, val protocol (conf .001, multi-label NMS)")
+                    if task else "mean |delta| of the Detect head maps with the conv alone in e4m3",
             "script": "scripts/fp8_calibrate.py"})
+        p._sessions.clear()
+        if task:  # task-aware ranking: each conv's own effect on the metric config 5 reports
+            cal.macs = {k: v for k, v in cal.macs.items()}
+            s16 = p.session(32, 640, 640, half=True, conf=0.25, iou=0.7)
+            d, c = s16(xc.cuda())
+            torch.cuda.synchronize()
+            cnt = c.cpu().tolist()
+            dets = [d[i, : cnt[i]].cpu() for i in range(32)]
+            cb = {"img": xc, "cls": torch.cat([t[:, 5] for t in dets]), "bboxes": torch.cat([t[:, :4] for t in dets]),
+                  "batch_idx": torch.cat([torch.full((len(t),), i) for i, t in enumerate(dets)])}
+            p._sessions.clear()
+            base = p.val(data=[cb], half=True, conf=0.001).box.map50
+            print(f"calibration set: fp16 mAP50 vs its own detections {base:.4f}", flush=True)
+            for k in sorted(cal.qs):
+                one = quant.Fp8Calibration({k: cal.qs[k]}, {k: cal.delta[k]}, macs={k: cal.macs[k]})
+                p._sessions.clear()
+                m = p.val(data=[cb], half=True, conf=0.001, fp8=True, fp8_calibration=one).box.map50
+                cal.sens[k] = base - m
+            p._sessions.clear()
         cal.save(CAL)
         print(f"saved {CAL.relative_to(ROOT)}: {len(cal.qs)} candidate convs", flush=True)
-        p._sessions.clear()
     cal = quant.Fp8Calibration.load(CAL)
     for k in sorted(cal.sens, key=cal.sens.get):
         print(f"   {k:28s} sens {cal.sens[k]:.4g}  MAC share {cal.macs[k] / sum(cal.macs.values()):.4f}")

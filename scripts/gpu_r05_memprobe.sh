@@ -27,3 +27,12 @@ for k, d in agg.items():
     for c, v in sorted(d.items()):
         print(f"   {c:36s} {sum(v) / len(v):16.0f}  (n={len(v)})")
 PY
+# halo tile-height / channel-slice A/B on the deep-K head 3x3 shapes (bs16 sub-batch graphs), two rounds
+for r in 1 2; do
+  for e in "-" "YDBL_HALO_TH=16" "YDBL_HALO_TH=20" "YDBL_HALO_TH=8 YDBL_HALO_NTN=4" "YDBL_HALO_TH=16 YDBL_HALO_NTN=4"; do
+    echo "== round $r env $e" >> $T/halo_ab.txt
+    if [ "$e" = "-" ]; then timeout -k 10 120 python scripts/kbench.py "k3s1@40 bs16" "k3s1@80 bs16" >> $T/halo_ab.txt 2>&1 || exit 1
+    else env $e timeout -k 10 120 python scripts/kbench.py "k3s1@40 bs16" "k3s1@80 bs16" >> $T/halo_ab.txt 2>&1 || exit 1; fi
+  done
+done
+cat $T/halo_ab.txt

@@ -71,3 +71,21 @@ def test_branch_plans_must_be_single_stream():
     with pytest.raises(RuntimeError, match="unflagged"):
         p.check_single_stream()
     assert _lib.lib.ydbl_detect_decode is p.steps[0].fn
+
+
+def test_switch_list_matches_sources():
+    """runtime.SWITCHES (the compiled-plan cache keys) names every YDBL_* environment switch the product reads."""
+    import re
+    from pathlib import Path
+
+    from ydbl.runtime import SWITCHES
+
+    root = Path(__file__).resolve().parents[1] / "yolo-dbl_amd"
+    read = set()
+    for f in [*root.glob("ydbl/**/*.py"), *root.glob("csrc/*.hip"), *root.glob("csrc/*.hpp")]:
+        t = f.read_text()
+        read |= set(re.findall(r'getenv\("(YDBL_[A-Z0-9_]+)"\)', t))
+        read |= set(re.findall(r'environ\.get\("(YDBL_[A-Z0-9_]+)"', t))
+        read |= set(re.findall(r'os\.environ\["(YDBL_[A-Z0-9_]+)"\]', t))
+    read -= {"YDBL_OFFLOAD_ARCH", "YDBL_LIB"}  # build / loader settings, not plan routing
+    assert read == set(SWITCHES), (read ^ set(SWITCHES))

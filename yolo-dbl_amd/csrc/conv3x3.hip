@@ -27,7 +27,20 @@ __device__ __forceinline__ int hslot(int pix, int g) {
   return (pix / (16 * S)) * (64 * S) + g * (16 * S) + (pix % S) * 16 + ((pix / S) & 15);
 }
 
-template <typename T, int S, int TH, int NTN, bool Q8>
+// Staging lane map (which 16-byte vector a lane loads for LDS slot group `c` of 64 slots): every vector is one
+// k-vector g (8 channels) of one pixel (halo) or weight row (weights); a pixel's / row's 4 k-vectors are one
+// contiguous 64-byte piece of global memory.
+//   MAP 0: lane L -> item L % 16, k-vector L / 16: 16 distinct 64-B pieces per 16 lanes
+//   MAP 1: lane L -> item (L & 3) + 4 (L >> 4), k-vector (L >> 2) & 3: every 16 lanes read 4 whole pieces
+//   MAP 2: lane L -> item L >> 2, k-vector L & 3: every 4 lanes read one whole piece
+template <int MAP>
+__device__ __forceinline__ void stage_item(int lane, int& item, int& gv) {
+  if constexpr (MAP == 0) { item = lane & 15; gv = lane >> 4; }
+  else if constexpr (MAP == 1) { item = (lane & 3) + 4 * (lane >> 4); gv = (lane >> 2) & 3; }
+  else { item = lane >> 2; gv = lane & 3; }
+}
+
+template <typename T, int S, int TH, int NTN, bool Q8, int MAP = 0>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int tiles_x, int tiles_y,
                                                               int co_splits) {
   constexpr int TW = 16;
@@ -64,26 +77,35 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   // source offsets are chunk-invariant and computed once.
   const T* xsrc[XIT];
   bool xok[XIT];
+  int xdst[XIT];  // LDS slot each staged halo vector goes to (-1: none)
 #pragma unroll
   for (int it = 0; it < XIT; ++it) {
-    const int slot = min(it * 256 + tid, XSLOTS - 1);
-    const int blk = slot / (64 * S), rem = slot % (64 * S);
-    const int gv = rem / (16 * S), r2 = rem % (16 * S);
-    const int px = blk * 16 * S + (r2 & 15) * S + r2 / 16;
+    // slot group c of 64 slots = 16 pixels x 4 k-vectors (pixels 16c .. 16c + 15 of the halo, in order)
+    const int c = it * 4 + (tid >> 6);
+    int item, gv;
+    stage_item<MAP>(lane, item, gv);
+    const int px = c * 16 + item;
     const int hy = px / IW, hx = px - hy * IW;
     const int iy = iy0 + hy, ix = ix0 + hx;
+    const int slot = hslot<S>(px, gv);
+    xdst[it] = slot < XSLOTS ? slot : -1;
     xok[it] = px < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-    xsrc[it] = p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + gv * VEC;
+    xsrc[it] = p.x + ((int64_t)(b * p.H + min(max(iy, 0), p.H - 1)) * p.W + min(max(ix, 0), p.W - 1)) * p.xcs +
+               gv * VEC;
   }
   int64_t wsrc[WIT];  // element offsets into the weight matrix
   bool wok[WIT];
+  int wdst[WIT];
 #pragma unroll
   for (int it = 0; it < WIT; ++it) {  // slot = ((cb*9 + tap)*4 + g)*16 + r  ->  row cb*16 + r
-    const int slot = min(it * 256 + tid, WV - 1);
-    const int r = slot & 15, gv = (slot >> 4) & 3, t2 = slot >> 6;
-    const int tap = t2 % 9, cb = t2 / 9;
+    const int c = it * 4 + (tid >> 6);  // slot group: 16 rows of one (cb, tap) x 4 k-vectors
+    int r, gv;
+    stage_item<MAP>(lane, r, gv);
+    const int tap = c % 9, cb = c / 9;
+    const int slot = (c * 4 + gv) * 16 + r;
+    wdst[it] = slot < WV ? slot : -1;
     const int co = co0 + cb * 16 + r;
-    wok[it] = co < p.Cout;
+    wok[it] = co < p.Cout && slot < WV;
     wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
   // raw loads, zero selects at the LDS store (vload_clamped): the next chunk stays in flight during the MFMAs
@@ -100,10 +122,10 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   auto store_chunk = [&]() {
 #pragma unroll
     for (int it = 0; it < XIT; ++it)
-      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
+      if (xdst[it] >= 0) s_x[xdst[it]] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
 #pragma unroll
     for (int it = 0; it < WIT; ++it)
-      if (it * 256 + tid < WV) s_w[it * 256 + tid] = vsel(wr[it], wok[it] && cok);
+      if (wdst[it] >= 0) s_w[wdst[it]] = vsel(wr[it], wok[it] && cok);
   };
 
   f32x4 acc[NTN][TMW];
@@ -158,8 +180,21 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co);
 }
 
+template <typename T, bool Q8, int S, int TH, int MAP = 0>
+static void launch_halo_map(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0);
+
+// YDBL_HALO_MAP=0|1|2: the staging lane map (stage_item) -- experiment switch
 template <typename T, bool Q8, int S, int TH>
-static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
+static void launch_halo(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0) {
+  const char* e = getenv("YDBL_HALO_MAP");
+  const int map = e ? atoi(e) : 0;
+  if (map == 1) launch_halo_map<T, Q8, S, TH, 1>(a, s, force_ntn);
+  else if (map == 2) launch_halo_map<T, Q8, S, TH, 2>(a, s, force_ntn);
+  else launch_halo_map<T, Q8, S, TH, 0>(a, s, force_ntn);
+}
+
+template <typename T, bool Q8, int S, int TH, int MAP>
+static void launch_halo_map(const ConvArgs<T>& a, hipStream_t s, int force_ntn) {
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
@@ -167,14 +202,20 @@ static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
   // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench)
   constexpr int64_t n2_below = 512;
+  if (force_ntn == 2 || force_ntn == 4) {
+    const int cs = (int)cdiv(a.Cout, force_ntn * 16);
+    if (force_ntn == 2) conv3x3_halo_kernel<T, S, TH, 2, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    else conv3x3_halo_kernel<T, S, TH, 4, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    return;
+  }
   if (a.Cout <= 32) {
-    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8, MAP><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
     const int cs = (int)cdiv(a.Cout, 32);
-    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   } else {
     const int cs = (int)cdiv(a.Cout, 64);
-    conv3x3_halo_kernel<T, S, TH, 4, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 4, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   }
 }
 
@@ -213,6 +254,14 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   (void)tiles8;
   // Cout <= 32 (one 32-channel slice: the weights are as many bytes per chunk as the halo): 16-row tiles from
   // 256 of them (DBL-n's 256->32 @80^2 at bs16, 400 tiles: 34.6 -> 31.8 us in graph, scripts/kbench.py)
+  // YDBL_HALO_TH=8|16|20 [YDBL_HALO_NTN=2|4]: experiment switch for tile-height / channel-slice A/Bs (kbench)
+  if (const char* e = getenv("YDBL_HALO_TH")) {
+    const char* f = getenv("YDBL_HALO_NTN");
+    const int th = atoi(e), ntn = f ? atoi(f) : 0;
+    if (th == 8) return launch_halo<T, Q8, 1, 8>(a, s, ntn), true;
+    if (th == 16) return launch_halo<T, Q8, 1, 16>(a, s, ntn), true;
+    if (th == 20) return launch_halo<T, Q8, 1, 20>(a, s, ntn), true;
+  }
   if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256)) launch_halo<T, Q8, 1, 16>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);
   return true;

@@ -75,6 +75,31 @@ def check_tensor_source(im, stride: int = 32) -> torch.Tensor:
     return im
 
 
+_SCALES = {}
+
+
+def _scale_consts(dev):
+    """(1.0, fp32(1/255)) as 0-dim fp32 tensors on `dev` (made once)."""
+    c = _SCALES.get(dev)
+    if c is None:
+        c = _SCALES[dev] = (torch.ones((), dtype=torch.float32, device=dev),
+                            torch.full((), 1.0 / 255.0, dtype=torch.float32, device=dev))
+    return c
+
+
+class _LazyHWC:
+    """Per-image HWC views of a batch, scaled by a 0-dim device tensor, made on first access (Results.orig_img)."""
+
+    def __init__(self, im, scale):
+        self.im, self.scale, self.hwc = im, scale, None
+
+    def __getitem__(self, i):
+        if self.hwc is None:
+            x = self.im.float() if self.scale is None else self.im * self.scale
+            self.hwc = x.permute(0, 2, 3, 1)
+        return self.hwc[i]
+
+
 class Model:
     """U/engine/model.py:84-643 (detect task subset)."""
 
@@ -238,33 +263,36 @@ class Model:
                 return self._predict_frames(frames, args, dev, t0, stream, paths)
             raise TypeError(f"unsupported source type {type(source).__name__}")
         im = check_tensor_source(source, int(self.model.stride.max()))
-        big = None
-        if im.device == dev:  # LoadTensor's /255 rule, on the tensor's device: the reduction runs during the lookup
-            big = im.amax() > 1.0 + (torch.finfo(im.dtype).eps if im.is_floating_point() else 0.0)
+        scale = None
+        if im.device == dev:
+            # LoadTensor's /255 rule on the tensor's device without a host sync: the session's input copy multiplies
+            # by fp32(1/255) when max > 1 (torch's GPU x / 255.0 is exactly that product), by 1 otherwise
+            one, inv = _scale_consts(dev)
+            scale = torch.where(im.amax() > 1.0 + (torch.finfo(im.dtype).eps if im.is_floating_point() else 0.0),
+                                inv, one)
         else:  # host tensors are scaled on the host, where the reference's LoadTensor does it, then moved
-            im = load_tensor_source(im).to(dev, non_blocking=True)
+            im = load_tensor_source(im).to(dev, non_blocking=True).float()
         b, _, h, w = im.shape
         s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
                          agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
                          streams=args["streams"], fp8_calibration=args["fp8_calibration"])
-        im = im.float() / 255.0 if big is not None and bool(big) else im.float()
         t1 = time.perf_counter()
-        det, cnt = s(im)
+        det, cnt = s(im, scale)
         if self._stale(s):  # weights edited since the session was compiled: rebuild and run again
             det, cnt = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"],
                                     max_det=args["max_det"], agnostic=args["agnostic_nms"], classes=args["classes"],
                                     device=dev, fp8=args["fp8"], streams=args["streams"],
-                                    fp8_calibration=args["fp8_calibration"])(im)
+                                    fp8_calibration=args["fp8_calibration"])(im, scale)
         counts = cnt.tolist()  # one sync per batch
         t2 = time.perf_counter()
         speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b, "postprocess": 0.0}
         # one copy of the batch's detections (the session's buffers are reused by the next call); each image's
         # boxes are a view of it, and orig_img a view of the input batch (HWC, as LoadTensor hands it over)
         dets = det[:, : max(counts, default=0)].clone()
-        hwc = im.permute(0, 2, 3, 1)
-        names = self.model.names
-        results = [Results(hwc[i], path=f"image{i}.jpg", names=names, boxes=dets[i, : counts[i]], speed=speed)
-                   for i in range(b)]
+        hwc = _LazyHWC(im, scale)  # orig_img: the LoadTensor-scaled image, HWC, computed on first access
+        names, shape = self.model.names, (h, w)
+        results = [Results(lambda i=i: hwc[i], path=f"image{i}.jpg", names=names, speed=speed, orig_shape=shape,
+                           boxes=lambda i=i, c=c: dets[i, :c]) for i, c in enumerate(counts)]
         return iter(results) if stream else results
 
     def _predict_frames(self, frames, args, dev, t0, stream, paths=None):

@@ -121,13 +121,38 @@ class Boxes:
 class Results:
     """U/engine/results.py:187- (detection subset: boxes, names, orig_shape, speed)."""
 
-    def __init__(self, orig_img, path, names, boxes=None, speed=None):
-        self.orig_img = orig_img
-        self.orig_shape = tuple(orig_img.shape[:2]) if orig_img is not None else None
+    def __init__(self, orig_img, path, names, boxes=None, speed=None, orig_shape=None):
+        """orig_img / boxes may also be zero-argument callables producing them (predict() hands over per-image views
+        of its batch buffers that way: built on first access, not for every image of every batch)."""
+        self._orig_img = orig_img
+        if orig_shape is None and orig_img is not None:
+            orig_shape = (orig_img() if callable(orig_img) else orig_img).shape[:2]
+        self.orig_shape = tuple(orig_shape) if orig_shape is not None else None
         self.path = path
         self.names = names
-        self.boxes = Boxes(boxes, self.orig_shape) if boxes is not None else None
+        self._boxes_src, self._boxes = boxes, None
         self.speed = speed or {"preprocess": None, "inference": None, "postprocess": None}
+
+    @property
+    def orig_img(self):
+        if callable(self._orig_img):
+            self._orig_img = self._orig_img()
+        return self._orig_img
+
+    @orig_img.setter
+    def orig_img(self, v):
+        self._orig_img = v
+
+    @property
+    def boxes(self):
+        if self._boxes is None and self._boxes_src is not None:
+            src = self._boxes_src() if callable(self._boxes_src) else self._boxes_src
+            self._boxes, self._boxes_src = Boxes(src, self.orig_shape), None
+        return self._boxes
+
+    @boxes.setter
+    def boxes(self, v):
+        self._boxes, self._boxes_src = v, None
 
     def __len__(self):
         return 0 if self.boxes is None else len(self.boxes)
@@ -142,7 +167,7 @@ class Results:
         return r
 
     def new(self):
-        return Results(self.orig_img, self.path, self.names, None, self.speed)
+        return Results(self._orig_img, self.path, self.names, None, self.speed, orig_shape=self.orig_shape)
 
     def update(self, boxes=None):
         """U/engine/results.py:308-334 (boxes): clip to the original image and replace."""

@@ -154,17 +154,22 @@ class DetectSession:
         self._cand_count = v
 
     # ------------------------------------------------------------------ execution
-    def load(self, x: torch.Tensor):
-        """Copy a BCHW float batch into the static input buffer (LoadTensor semantics are the caller's)."""
+    def load(self, x: torch.Tensor, scale: torch.Tensor | None = None):
+        """Copy a BCHW batch into the static input buffer (LoadTensor semantics are the caller's); scale: a 0-dim
+        fp32 device tensor the batch is multiplied by on the way in (predict()'s /255 decision, taken on the device:
+        x * fp32(1/255) is what torch's GPU division by 255.0 computes, so no host sync is needed for it)."""
         if self.children:
             if tuple(x.shape[1:]) != (3, self.h, self.w) or x.shape[0] != self.batch:
                 raise ValueError(f"input shape {tuple(x.shape)} != session shape {(self.batch, 3, self.h, self.w)}")
             for c, (a, b) in zip(self.children, self.bounds):
-                c.load(x[a:b])
+                c.load(x[a:b], scale)
             return
         if tuple(x.shape) != tuple(self.compiled.input.shape):
             raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
-        self.compiled.input.copy_(x, non_blocking=True)
+        if scale is None:
+            self.compiled.input.copy_(x, non_blocking=True)
+        else:
+            torch.mul(x, scale, out=self.compiled.input)
 
     def calibrate_fp8(self, x: torch.Tensor | None = None, fraction: float | None = None, calibration=None) -> int:
         """Switch the dense convs to e4m3 operands (ydbl.quant).  calibration (an ydbl.quant.Fp8Calibration or the
@@ -229,9 +234,9 @@ class DetectSession:
         else:
             self.plan.run()
 
-    def __call__(self, x: torch.Tensor | None = None):
+    def __call__(self, x: torch.Tensor | None = None, scale: torch.Tensor | None = None):
         if x is not None:
-            self.load(x)
+            self.load(x, scale)
         self.launch()
         return self.det, self.count
 

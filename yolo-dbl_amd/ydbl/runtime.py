@@ -22,10 +22,19 @@ from . import _lib
 from ._lib import View, lib
 
 
+# The YDBL_* switches that change what a plan builds or launches (plan-builder fusions in ydbl.nn.modules / tasks,
+# routing in the C-ABI, read at build or at each launch).  tests/test_host_api.py checks this list against the
+# names the sources read.
+SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_HALO_MAP", "YDBL_HALO_NTN", "YDBL_HALO_TH", "YDBL_HG_UNFUSED",
+            "YDBL_LSK_UNFUSED", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_NO_BNECK", "YDBL_NO_CV1_FUSE",
+            "YDBL_NO_CV3_FUSE", "YDBL_NO_FUSE_PAD", "YDBL_NO_MERGE", "YDBL_NO_STEM2")
+
+
 def ydbl_env() -> tuple:
-    """The YDBL_* switches (plan-builder fusions, C-ABI routing), read when a plan is built or launched: part of
-    every compiled-plan cache key."""
-    return tuple(sorted((k, v) for k, v in os.environ.items() if k.startswith("YDBL_")))
+    """The settings of the YDBL_* switches (SWITCHES): part of every compiled-plan cache key, since a captured
+    graph keeps the routing of its capture.  (~5 us: the predict() hot path; a scan of os.environ took 100.)"""
+    get = os.environ.get
+    return tuple(get(k) for k in SWITCHES)
 
 
 _STRUCT_EPOCH = [0]  # bumped whenever any module registers a parameter, buffer or submodule (torch global hooks)
