@@ -483,8 +483,12 @@ def main():
     sp = ShardedPredictor(model, B * world, S, S, dev, half=half, conf=0.25, iou=0.7, max_det=300, fp8=fp8,
                           streams=args.streams)
     sess = sp.session
-    if args.fp8:  # activation scales from a separate synthetic calibration batch
-        sess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
+    fp8_cal = fp8_calibration_file(cfg)
+    if args.fp8:  # the committed calibration of these weights (one layer set per share), else a calibration batch
+        if fp8_cal is not None:
+            sess.calibrate_fp8(calibration=fp8_cal)
+        else:
+            sess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
     # synthetic images, different per rank, resident in the session's input buffer (HBM)
     sp.load(images_local=blob_images(B, S, seed=1234 + rank).to(dev))
 
@@ -508,7 +512,9 @@ def main():
         rsess, rkey = sess, key
         if args.streams > 1:
             rsess = model.session(B, S, S, half=half, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=fp8, streams=1)
-            if args.fp8:
+            if args.fp8 and fp8_cal is not None:
+                rsess.calibrate_fp8(calibration=fp8_cal)
+            elif args.fp8:
                 rsess.calibrate_fp8(blob_images(B, S, seed=4321 + rank).to(dev))
             rsess.load(blob_images(B, S, seed=1234 + rank).to(dev))
             rsess()
@@ -524,6 +530,12 @@ def main():
         dist.destroy_process_group()
 
 
+def fp8_calibration_file(cfg):
+    """The committed fp8 calibration of the fixture weights of `cfg` (scripts/fp8_calibrate.py), if any."""
+    f = ROOT / "tests" / "golden" / f"fp8_calib_{Path(cfg).stem}_nc3.json"
+    return str(f) if f.exists() else None
+
+
 def predict_main(args, model, world, rank, dev, half, fp8, dtype_name, cfg):
     """--via-predict: the step is the user-facing call YOLO.predict(x, half=...) on this rank's HBM-resident
     batch, with predict()'s own stream layout (ydbl.engine.session.default_streams: the split hipGraph from
@@ -532,8 +544,8 @@ def predict_main(args, model, world, rank, dev, half, fp8, dtype_name, cfg):
 
     B, S = args.batch, args.imgsz
     x = blob_images(B, S, seed=1234 + rank).to(dev)
-    kw = dict(half=half, fp8=fp8, conf=0.25, iou=0.7, max_det=300, device=dev)
-    if fp8:  # calibrate once on the separate synthetic batch, as the session bench does
+    kw = dict(half=half, fp8=fp8, conf=0.25, iou=0.7, max_det=300, device=dev, fp8_calibration=fp8_calibration_file(cfg))
+    if fp8 and kw["fp8_calibration"] is None:  # calibrate once on the separate synthetic batch, as the session bench
         from ydbl.engine.session import default_streams
 
         model.session(B, S, S, half=True, conf=0.25, iou=0.7, max_det=300, device=dev, fp8=fp8,

@@ -1225,3 +1225,46 @@ def test_lsk_fused_bit_identical(c, shape, sliced, monkeypatch):
     with torch.no_grad():
         ref = o(x)
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("ring", ["8", "16", "20", "16,8", "20,8"])
+@pytest.mark.parametrize("n,cin,cout,h,w,res", [
+    (16, 384, 64, 40, 40, None),      # the bench's head Bottleneck cv1 (bs16 sub-batch graph)
+    (16, 256, 32, 80, 80, None),      # Detect cv2 at P3
+    (3, 192, 48, 40, 40, "add"),      # partial second channel slice, residual, few images
+    (2, 64, 128, 24, 40, None),       # two chunks only; ragged row and column tiles
+])
+def test_conv3x3_ring(monkeypatch, ring, n, cin, cout, h, w, res):
+    """The LDS-DMA ring kernel (csrc/conv3x3_ring.hip, YDBL_HALO_RING=TH[,WAVES]) against fp32 F.conv2d, and bit for
+    bit against the register-staged halo kernel (same fragments, same accumulation order per output)."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + cout + h + 7)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.half().float(), wt.half().float(), b, 1, 1))
+    outs = []
+    for route in (ring, None):
+        if route is None:
+            monkeypatch.delenv("YDBL_HALO_RING", raising=False)
+        else:
+            monkeypatch.setenv("YDBL_HALO_RING", route)
+        plan = _plan(torch.float16)
+        xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+        ybuf = plan.alloc(n, h, w, cout + 8)
+        yv = ybuf.cslice(8, cout)
+        rv, mode = None, _lib.RES_NONE
+        if res:
+            r = torch.randn(n, cout, h, w, generator=torch.Generator().manual_seed(5))
+            rv = _tv_from_nchw(plan, r)
+            mode = _lib.RES_ADD
+        emit_dense(plan, xv, yv, wt, b, 1, 1, 1, _lib.ACT_SILU, rv, mode)
+        _run(plan)
+        outs.append(yv.nchw().float().cpu())
+        if res:
+            ref_r = r.half().float() + ref
+    torch.testing.assert_close(outs[0], ref_r if res else ref, rtol=3e-2, atol=3e-2)
+    if n * h * w >= 25600:  # (smaller maps take the block GEMM without the ring: no bitwise twin)
+        assert torch.equal(outs[0], outs[1])

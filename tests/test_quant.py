@@ -71,3 +71,6 @@ def test_calibration_roundtrip_and_shares(tmp_path):
     assert back.switched(1.0) == ["a", "b", "c"]
     assert back.switched(0.3) == ["c"]  # b (least sensitive) is 60 % of the MACs: skipped, c fits
     assert back.switched(0.95) == ["b", "c"] and abs(back.mac_fraction(["b", "c"]) - 0.9) < 1e-12
+    cal.sets = {"0.25": ["a"]}  # an explicit set recorded for a share wins over the ranking's budget pick
+    back = Fp8Calibration.load(cal.save(tmp_path / "cal2.json"))
+    assert back.switched(0.25) == ["a"] and back.switched(0.3) == ["c"]

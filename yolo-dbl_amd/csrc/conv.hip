@@ -613,6 +613,7 @@ template <typename T, bool Q8>
 static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
   if constexpr (sizeof(T) == 2 && !Q8) {
     if (try_conv3x3_vw(a, kh, s)) return;
+    if (try_conv3x3_ring(a, kh, s)) return;
   }
   if (!Q8 && try_tile<T>(a, kh, s)) return;
   if (try_conv3x3_halo<T, Q8>(a, kh, s)) return;

@@ -22,40 +22,24 @@
 
 namespace ydbl {
 
-template <int S>
-__device__ __forceinline__ int hslot(int pix, int g) {
-  return (pix / (16 * S)) * (64 * S) + g * (16 * S) + (pix % S) * 16 + ((pix / S) & 15);
-}
 
-// Staging lane map (which 16-byte vector a lane loads for LDS slot group `c` of 64 slots): every vector is one
-// k-vector g (8 channels) of one pixel (halo) or weight row (weights); a pixel's / row's 4 k-vectors are one
-// contiguous 64-byte piece of global memory.
-//   MAP 0: lane L -> item L % 16, k-vector L / 16: 16 distinct 64-B pieces per 16 lanes
-//   MAP 1: lane L -> item (L & 3) + 4 (L >> 4), k-vector (L >> 2) & 3: every 16 lanes read 4 whole pieces
-//   MAP 2: lane L -> item L >> 2, k-vector L & 3: every 4 lanes read one whole piece
-template <int MAP>
-__device__ __forceinline__ void stage_item(int lane, int& item, int& gv) {
-  if constexpr (MAP == 0) { item = lane & 15; gv = lane >> 4; }
-  else if constexpr (MAP == 1) { item = (lane & 3) + 4 * (lane >> 4); gv = (lane >> 2) & 3; }
-  else { item = lane >> 2; gv = lane & 3; }
-}
-
-template <typename T, int S, int TH, int NTN, bool Q8, int MAP = 0>
+template <typename T, int S, int TH, int NTN, bool Q8, int KS = 1>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int tiles_x, int tiles_y,
-                                                              int co_splits) {
+                                                              int co_splits, int diag = 0) {
+  // KS k-steps (of BK channels each) per chunk: one global round trip and two barriers per KS * BK channels
   constexpr int TW = 16;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;
   constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   constexpr int NPIX = IH * IW;
   constexpr int XSLOTS = (NPIX + 16 * S - 1) / (16 * S) * (64 * S);
-  constexpr int WV = NTN * 16 * 36;  // weight vectors per chunk
+  constexpr int WV = NTN * 16 * 36;  // weight vectors per k-step
   constexpr int XIT = (XSLOTS + 255) / 256, WIT = (WV + 255) / 256;
   constexpr int TMW = (TH + 3) / 4;  // 16-pixel tiles (= output rows) per wave
   using vec = typename Vec<T>::type;
   using opv = typename Op<T, Q8>::lds;  // 8-byte e4m3 groups in fp8 mode (same slot layout)
-  __shared__ opv s_x[XSLOTS];
-  __shared__ opv s_w[WV];
+  __shared__ opv s_x[KS * XSLOTS];
+  __shared__ opv s_w[KS * WV];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -74,58 +58,71 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   // Staging walks LDS slots linearly (consecutive lanes -> consecutive 16-byte slots, so the
   // ds_write_b128s are conflict-free) and gathers the matching global vectors: a wave still
   // covers 16 pixels x 64 B (halo) / 16 rows x 64 B (weights) of global memory.  The per-lane
-  // source offsets are chunk-invariant and computed once.
+  // source offsets are chunk-invariant and computed once.  (Lane maps that read whole 64-byte pieces per
+  // lane quad cut the TCP accesses 3.2x and TD busy 1.7x but not the time: 384->64 @40^2 bs16 29.6 vs 30.2 us,
+  // profiles/r05/r05_halo_lane_map_ab.txt.)
   const T* xsrc[XIT];
   bool xok[XIT];
-  int xdst[XIT];  // LDS slot each staged halo vector goes to (-1: none)
 #pragma unroll
   for (int it = 0; it < XIT; ++it) {
-    // slot group c of 64 slots = 16 pixels x 4 k-vectors (pixels 16c .. 16c + 15 of the halo, in order)
-    const int c = it * 4 + (tid >> 6);
-    int item, gv;
-    stage_item<MAP>(lane, item, gv);
-    const int px = c * 16 + item;
+    const int slot = min(it * 256 + tid, XSLOTS - 1);
+    const int blk = slot / (64 * S), rem = slot % (64 * S);
+    const int gv = rem / (16 * S), r2 = rem % (16 * S);
+    const int px = blk * 16 * S + (r2 & 15) * S + r2 / 16;
     const int hy = px / IW, hx = px - hy * IW;
     const int iy = iy0 + hy, ix = ix0 + hx;
-    const int slot = hslot<S>(px, gv);
-    xdst[it] = slot < XSLOTS ? slot : -1;
     xok[it] = px < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-    xsrc[it] = p.x + ((int64_t)(b * p.H + min(max(iy, 0), p.H - 1)) * p.W + min(max(ix, 0), p.W - 1)) * p.xcs +
-               gv * VEC;
+    xsrc[it] = p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + gv * VEC;
   }
   int64_t wsrc[WIT];  // element offsets into the weight matrix
   bool wok[WIT];
-  int wdst[WIT];
 #pragma unroll
   for (int it = 0; it < WIT; ++it) {  // slot = ((cb*9 + tap)*4 + g)*16 + r  ->  row cb*16 + r
-    const int c = it * 4 + (tid >> 6);  // slot group: 16 rows of one (cb, tap) x 4 k-vectors
-    int r, gv;
-    stage_item<MAP>(lane, r, gv);
-    const int tap = c % 9, cb = c / 9;
-    const int slot = (c * 4 + gv) * 16 + r;
-    wdst[it] = slot < WV ? slot : -1;
+    const int slot = min(it * 256 + tid, WV - 1);
+    const int r = slot & 15, gv = (slot >> 4) & 3, t2 = slot >> 6;
+    const int tap = t2 % 9, cb = t2 / 9;
     const int co = co0 + cb * 16 + r;
-    wok[it] = co < p.Cout && slot < WV;
+    wok[it] = co < p.Cout;
     wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
   // raw loads, zero selects at the LDS store (vload_clamped): the next chunk stays in flight during the MFMAs
-  vec xr[XIT];
-  opv wr[WIT];
+  vec xr[KS][XIT];
+  opv wr[KS][WIT];
   bool cok = true;
+  // diag (timing-only experiment switch, wrong results): bit 0 = stage the weights of chunk 0 only, bit 1 = the
+  // halo of chunk 0 only, bit 2 = skip the MFMAs
+  const bool skip_w = diag & 1, skip_x = diag & 2;
+  bool first = true;
   auto load_chunk = [&](int c0) {
     cok = c0 < p.Cin;
 #pragma unroll
-    for (int it = 0; it < XIT; ++it) xr[it] = vload_clamped(xsrc[it] + c0, p.x, xok[it] && cok);
+    for (int k = 0; k < KS; ++k) {
+      if (!(skip_x && !first)) {
 #pragma unroll
-    for (int it = 0; it < WIT; ++it) wr[it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0, wok[it] && cok);
+        for (int it = 0; it < XIT; ++it) xr[k][it] = vload_clamped(xsrc[it] + c0 + k * BK, p.x, xok[it] && cok);
+      }
+      if (!(skip_w && !first)) {
+#pragma unroll
+        for (int it = 0; it < WIT; ++it) wr[k][it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0 + k * BK, wok[it] && cok);
+      }
+    }
   };
   auto store_chunk = [&]() {
 #pragma unroll
-    for (int it = 0; it < XIT; ++it)
-      if (xdst[it] >= 0) s_x[xdst[it]] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
+    for (int k = 0; k < KS; ++k) {
+      if (!(skip_x && !first)) {
 #pragma unroll
-    for (int it = 0; it < WIT; ++it)
-      if (wdst[it] >= 0) s_w[wdst[it]] = vsel(wr[it], wok[it] && cok);
+        for (int it = 0; it < XIT; ++it)
+          if (it * 256 + tid < XSLOTS)
+            s_x[k * XSLOTS + it * 256 + tid] = to_op<T, Q8>(vsel(xr[k][it], xok[it] && cok), p.qs);
+      }
+      if (!(skip_w && !first)) {
+#pragma unroll
+        for (int it = 0; it < WIT; ++it)
+          if (it * 256 + tid < WV) s_w[k * WV + it * 256 + tid] = vsel(wr[k][it], wok[it] && cok);
+      }
+    }
+    first = false;
   };
 
   f32x4 acc[NTN][TMW];
@@ -136,27 +133,31 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
 
   // one LDS buffer, refilled between barriers; the next chunk is in registers during the MFMAs (two buffers and
   // one barrier per chunk measured even or slower: kbench bs16 384->64 @40^2 27.0 vs 26.7 us, 64->128 13.2 vs 15.7)
-  const int nchunks = p.Cin / BK;
+  const int nchunks = p.Cin / (KS * BK);
   load_chunk(0);
   store_chunk();
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
-    if (ch + 1 < nchunks) load_chunk((ch + 1) * BK);
+    if (ch + 1 < nchunks) load_chunk((ch + 1) * KS * BK);  // (after chunk 0's store: `first` is false)
+    if (!(diag & 4))  // diag bit 2: no MFMAs (staging and barriers alone)
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap % 3;
-      opv af[NTN], bf[TMW];
 #pragma unroll
-      for (int i = 0; i < NTN; ++i) af[i] = s_w[((i * 9 + tap) * 4 + g) * 16 + r16];
+      for (int k = 0; k < KS; ++k) {
+        opv af[NTN], bf[TMW];
 #pragma unroll
-      for (int j = 0; j < TMW; ++j) {
-        const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
-        bf[j] = s_x[hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
+        for (int i = 0; i < NTN; ++i) af[i] = s_w[k * WV + ((i * 9 + tap) * 4 + g) * 16 + r16];
+#pragma unroll
+        for (int j = 0; j < TMW; ++j) {
+          const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
+          bf[j] = s_x[k * XSLOTS + hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
+        }
+#pragma unroll
+        for (int j = 0; j < TMW; ++j)
+#pragma unroll
+          for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
       }
-#pragma unroll
-      for (int j = 0; j < TMW; ++j)
-#pragma unroll
-        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
     }
     if (ch + 1 < nchunks) {
       __syncthreads();  // every wave is done reading this chunk
@@ -180,21 +181,22 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co);
 }
 
-template <typename T, bool Q8, int S, int TH, int MAP = 0>
-static void launch_halo_map(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0);
+template <typename T, bool Q8, int S, int TH, int KS = 1>
+static void launch_halo_ks(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0);
 
-// YDBL_HALO_MAP=0|1|2: the staging lane map (stage_item) -- experiment switch
+// YDBL_HALO_KS=1|2: k-steps per staged chunk -- experiment switch
 template <typename T, bool Q8, int S, int TH>
 static void launch_halo(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0) {
-  const char* e = getenv("YDBL_HALO_MAP");
-  const int map = e ? atoi(e) : 0;
-  if (map == 1) launch_halo_map<T, Q8, S, TH, 1>(a, s, force_ntn);
-  else if (map == 2) launch_halo_map<T, Q8, S, TH, 2>(a, s, force_ntn);
-  else launch_halo_map<T, Q8, S, TH, 0>(a, s, force_ntn);
+  constexpr int BK = 4 * Vec<T>::N;
+  const char* e = getenv("YDBL_HALO_KS");
+  if (e && atoi(e) == 2 && a.Cin % (2 * BK) == 0) launch_halo_ks<T, Q8, S, TH, 2>(a, s, force_ntn);
+  else launch_halo_ks<T, Q8, S, TH, 1>(a, s, force_ntn);
 }
 
-template <typename T, bool Q8, int S, int TH, int MAP>
-static void launch_halo_map(const ConvArgs<T>& a, hipStream_t s, int force_ntn) {
+template <typename T, bool Q8, int S, int TH, int KS>
+static void launch_halo_ks(const ConvArgs<T>& a, hipStream_t s, int force_ntn) {
+  const char* de = getenv("YDBL_HALO_DIAG");  // timing-only experiment switch (wrong results): see the kernel
+  const int diag = de ? atoi(de) : 0;
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
@@ -202,20 +204,22 @@ static void launch_halo_map(const ConvArgs<T>& a, hipStream_t s, int force_ntn) 
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
   // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench)
   constexpr int64_t n2_below = 512;
-  if (force_ntn == 2 || force_ntn == 4) {
+  if (force_ntn == 1 || force_ntn == 2 || force_ntn == 4) {
     const int cs = (int)cdiv(a.Cout, force_ntn * 16);
-    if (force_ntn == 2) conv3x3_halo_kernel<T, S, TH, 2, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
-    else conv3x3_halo_kernel<T, S, TH, 4, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    const unsigned grid = (unsigned)(ntiles * cs);
+    if (force_ntn == 1) conv3x3_halo_kernel<T, S, TH, 1, Q8, KS><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
+    else if (force_ntn == 2) conv3x3_halo_kernel<T, S, TH, 2, Q8, KS><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
+    else conv3x3_halo_kernel<T, S, TH, 4, Q8, KS><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
     return;
   }
   if (a.Cout <= 32) {
-    conv3x3_halo_kernel<T, S, TH, 2, Q8, MAP><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8, KS><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1, diag);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
     const int cs = (int)cdiv(a.Cout, 32);
-    conv3x3_halo_kernel<T, S, TH, 2, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8, KS><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
   } else {
     const int cs = (int)cdiv(a.Cout, 64);
-    conv3x3_halo_kernel<T, S, TH, 4, Q8, MAP><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+    conv3x3_halo_kernel<T, S, TH, 4, Q8, KS><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
   }
 }
 
@@ -254,13 +258,13 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   (void)tiles8;
   // Cout <= 32 (one 32-channel slice: the weights are as many bytes per chunk as the halo): 16-row tiles from
   // 256 of them (DBL-n's 256->32 @80^2 at bs16, 400 tiles: 34.6 -> 31.8 us in graph, scripts/kbench.py)
-  // YDBL_HALO_TH=8|16|20 [YDBL_HALO_NTN=2|4]: experiment switch for tile-height / channel-slice A/Bs (kbench)
+  // YDBL_HALO_TH=4|8|16 [YDBL_HALO_NTN=1|2|4]: experiment switch for tile-height / channel-slice A/Bs (kbench)
   if (const char* e = getenv("YDBL_HALO_TH")) {
     const char* f = getenv("YDBL_HALO_NTN");
     const int th = atoi(e), ntn = f ? atoi(f) : 0;
     if (th == 8) return launch_halo<T, Q8, 1, 8>(a, s, ntn), true;
     if (th == 16) return launch_halo<T, Q8, 1, 16>(a, s, ntn), true;
-    if (th == 20) return launch_halo<T, Q8, 1, 20>(a, s, ntn), true;
+    if (th == 4) return launch_halo<T, Q8, 1, 4>(a, s, ntn), true;
   }
   if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256)) launch_halo<T, Q8, 1, 16>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);

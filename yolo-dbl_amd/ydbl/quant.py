@@ -141,14 +141,19 @@ class Fp8Calibration:
     sensitive first): one calibration file = one layer set per share, whatever batch the model then runs.
     ``save`` / ``load``: JSON (committed for the fixture weights under tests/golden/)."""
 
-    def __init__(self, qs, delta, sens=None, macs=None, meta=None):
+    def __init__(self, qs, delta, sens=None, macs=None, meta=None, sets=None):
         self.qs, self.delta = dict(qs), {k: [float(v) for v in d] for k, d in delta.items()}
         self.sens, self.macs, self.meta = dict(sens or {}), dict(macs or {}), dict(meta or {})
+        self.sets = {str(k): sorted(v) for k, v in (sets or {}).items()}  # share -> explicit layer set
 
     def switched(self, fraction: float) -> list[str]:
+        """The layer set of a MAC share: an explicit set recorded for that share (sets, e.g. a greedy search), else
+        the least sensitive convs within the MAC budget (select_by_mac_budget)."""
         keys = sorted(self.qs)
         if fraction >= 1.0:
             return keys
+        if f"{fraction:g}" in self.sets:
+            return list(self.sets[f"{fraction:g}"])
         if not self.sens:
             raise ValueError("this calibration has no sensitivity ranking: only fraction 1.0 applies")
         chosen, _ = select_by_mac_budget([self.sens[k] for k in keys], [self.macs[k] for k in keys], fraction)
@@ -160,13 +165,13 @@ class Fp8Calibration:
 
     def to_json(self) -> dict:
         return {"format": "ydbl-fp8-calibration-1", "meta": self.meta, "qs": self.qs, "delta": self.delta,
-                "sens": self.sens, "macs": self.macs}
+                "sens": self.sens, "macs": self.macs, "sets": self.sets}
 
     @classmethod
     def from_json(cls, d):
         if d.get("format") != "ydbl-fp8-calibration-1":
             raise ValueError("not a ydbl fp8 calibration file")
-        return cls(d["qs"], d["delta"], d.get("sens"), d.get("macs"), d.get("meta"))
+        return cls(d["qs"], d["delta"], d.get("sens"), d.get("macs"), d.get("meta"), d.get("sets"))
 
     def save(self, path):
         import json
