@@ -144,6 +144,14 @@ typedef struct {
   int32_t g0_act;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
+/* Experiment (YDBL_DSC3K_CHAIN=1, ydbl.nn.modules.C3): DSC3k's two DSBottlenecks at 128 channels (block.py:1408-1503:
+ * k3 DSConv, k7 DSConv + x, k3 DSConv, k7 DSConv + x with cv3 as the trailing GEMM) as ONE launch over 8x8 tiles, the
+ * tiles of an image walking the four stages with a per-image group barrier between them; outputs bit-identical to
+ * the four ydbl_dsconv_nhwc launches.  d: those four descriptors in order; at most 160 tiles in all.  sync: 2*N + 1
+ * zeroed uint32 (left zeroed by the kernel; sync[2N] = 1 if a group barrier timed out).  stamps: NULL, or
+ * [N * tiles][4 stages][start, done, barrier passed] uint64 s_memrealtime values (100 MHz).  xcd_local: group barriers
+ * without L2 write-back / invalidate, relying on each image's tiles running on one XCD (used when N % 8 == 0). */
+int ydbl_dsc3k_chain(const ydbl_dsconv_desc* d, uint32_t* sync, uint64_t* stamps, int32_t xcd_local, void* stream);
 
 /* Depthwise convolution (groups = C), fp32 arithmetic.
  * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).

@@ -1,7 +1,7 @@
 """A/B of YDBL_* routing knobs on the bench workload in ONE process (same box, interleaved rounds), so box-to-box
 spread does not enter the comparison.  Each variant is a separate session (the session key holds the knobs).
 
-    python scripts/ab_bench.py "A:" "B:YDBL_NO_CV3_FUSE=1" [--model n] [--batch 32] [--streams 2] [--rounds 5]
+    python scripts/ab_bench.py "A:" "B:YDBL_NO_CV3_FUSE=1;YDBL_NO_MERGE=1" [--model n] [--batch 32] [--streams 2] [--rounds 5]
 """
 import argparse
 import os
@@ -20,7 +20,7 @@ from bench import CFGS  # noqa: E402
 
 def parse(spec):
     name, _, rest = spec.partition(":")
-    env = dict(kv.split("=", 1) for kv in rest.split(",") if kv)
+    env = dict(kv.split("=", 1) for kv in rest.split(";") if kv)  # K=V;K2=V2 (values may hold commas)
     return name, env
 
 

@@ -1,4 +1,5 @@
 # Same-box A/B of two builds of libydbl.so: the in-tree library vs abtmp/libydbl_base.so (YDBL_LIB), over
+set -o pipefail
 # scripts/kbench.py shapes (filters as arguments) and bench.py DBL-n bs32, twice each, alternating; plus the
 # GPU parity tests named by $PARITY (pytest -k expression) on the in-tree library first.
 # usage: PARITY="stem2 or bottleneck" bash scripts/gpu_lib_ab.sh TAG "kbench filter" ...

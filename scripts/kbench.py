@@ -131,6 +131,16 @@ def case_pair(B, cin, co, H, tail=False):
     return f"pair {cin}->{co}{'+tail' if tail else ''}@{H} bs{B}", build
 
 
+def case_dsc3k(B, c, H):
+    def build():
+        p = Plan(torch.device("cuda"), torch.float16)
+        x = p.alloc(B, H, H, c)
+        rnd(p, x)
+        M.DSC3k(c, c, n=2, e=1.0, k1=3, k2=7).eval().emit(p, x)
+        return p
+    return f"dsc3k {c}@{H} bs{B}", build
+
+
 def case_hg(B, c, H, edges=8):
     def build():
         p = Plan(torch.device("cuda"), torch.float16)
@@ -151,7 +161,7 @@ def case_dysample(B, c, H):
     return f"dysample {c}@{H} bs{B}", build
 
 
-CASES = [case_hg(16, 64, 40), case_hg(16, 128, 40), case_dysample(16, 128, 40), case_dysample(16, 256, 20), case_stem2(16), case_box3(16, 64, 80), case_box3(16, 128, 40), case_pair(16, 64, 64, 80),
+CASES = [case_dsc3k(16, 128, 20), case_hg(16, 64, 40), case_hg(16, 128, 40), case_dysample(16, 128, 40), case_dysample(16, 256, 20), case_stem2(16), case_box3(16, 64, 80), case_box3(16, 128, 40), case_pair(16, 64, 64, 80),
          case_pair(16, 64, 64, 80, True), case_pair(16, 128, 64, 40), case_pair(16, 256, 64, 20),
          case_dsconv(16, 128, 128, 3, 2, 80, 80), case_conv(16, 16, 32, 3, 2, 320, 320),
          case_conv(16, 32, 64, 3, 2, 160, 160), case_bneck(16, 32, 160),case_gate(16, 8, 8, 64), case_gate(16, 40, 40, 64),

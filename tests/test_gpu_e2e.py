@@ -143,11 +143,12 @@ def test_e2e_fp16(golden_dir, name, batch, streams):
     assert len(m["mismatches"]) <= 2 * o16["det_mismatches"] + 2, m["mismatches"][:5]
 
 
-@pytest.mark.parametrize("fraction", [0.25, 1.0])
+@pytest.mark.parametrize("fraction", [0.1, 0.25, 1.0])
 def test_e2e_fp8_config5(golden_dir, fraction):
     """BASELINE config 5 end to end at its own batch and the bench layout: DBL-s 640, bs 32, two sub-batch
-    streams, e4m3 operands on `fraction` of the candidate MACs (0.25 = the bench's config-5 setting, 1.0 = all),
-    one joint calibration on a separate batch (bench.py).  The reference has no fp8 path, so the bound is
+    streams, e4m3 operands on `fraction` of the candidate MACs (0.1 = the config-5 setting, DESIGN.md §4.1;
+    1.0 = all), with the committed calibration (tests/golden/fp8_calib_yolov13s_DBL_nc3.json: its scales, bias
+    corrections and the share's layer set, as bench.py --fp8 loads it).  The reference has no fp8 path, so the bound is
     derived the fp16 rule's way from the fp8 leg of the reference computation itself: the oracle's fp16 leg
     with the very layers the GPU switched emulated in e4m3 at the GPU's scales (parity_util.fp8_emulated_leg).
     GPU box / score deviation from fp64 (max, p99.9) <= 2x that leg's + the fp16 rule's floors; final
@@ -159,11 +160,15 @@ def test_e2e_fp8_config5(golden_dir, fraction):
     x = blob_images(meta["batch_full"], S, seed=meta["seed"])
     assert x.shape[0] == 32
     p, o = build_pair("s", 3, golden_dir)
+    from ydbl.quant import Fp8Calibration
+
+    cal = Fp8Calibration.load(golden_dir / "fp8_calib_yolov13s_DBL_nc3.json")
     s = p.session(32, S, S, half=True, conf=conf, iou=iou, keep_pred=True, fp8=True if fraction >= 1 else fraction,
-                  streams=2)
-    s.calibrate_fp8(blob_images(32, S, seed=4321).cuda())
+                  streams=2, fp8_calibration=cal)
     s(x.cuda())
     torch.cuda.synchronize()
+    if fraction < 1:
+        assert s.fp8_mac_fraction == pytest.approx(cal.mac_fraction(cal.switched(fraction)), abs=1e-6)
     yg = s.pred.cpu()[ref]  # ref spans both sub-batch graphs (images 0, 1, 15 | 16, 31)
     dets = [s.results()[i] for i in ref]
     assert [c.plan.fp8_switched for c in s.children][0] == s.children[1].plan.fp8_switched  # one joint selection

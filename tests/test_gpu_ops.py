@@ -1227,44 +1227,35 @@ def test_lsk_fused_bit_identical(c, shape, sliced, monkeypatch):
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("ring", ["8", "16", "20", "16,8", "20,8"])
-@pytest.mark.parametrize("n,cin,cout,h,w,res", [
-    (16, 384, 64, 40, 40, None),      # the bench's head Bottleneck cv1 (bs16 sub-batch graph)
-    (16, 256, 32, 80, 80, None),      # Detect cv2 at P3
-    (3, 192, 48, 40, 40, "add"),      # partial second channel slice, residual, few images
-    (2, 64, 128, 24, 40, None),       # two chunks only; ragged row and column tiles
-])
-def test_conv3x3_ring(monkeypatch, ring, n, cin, cout, h, w, res):
-    """The LDS-DMA ring kernel (csrc/conv3x3_ring.hip, YDBL_HALO_RING=TH[,WAVES]) against fp32 F.conv2d, and bit for
-    bit against the register-staged halo kernel (same fragments, same accumulation order per output)."""
-    from ydbl import _lib
-    from ydbl.nn.modules import emit_dense
+@pytest.mark.parametrize("n,h,w", [(16, 20, 20), (3, 20, 20), (8, 12, 20), (1, 8, 8)])
+def test_dsc3k_chain_bit_identical(monkeypatch, n, h, w):
+    """The DSC3k bottleneck pair at 128 channels as one launch with per-image group barriers (csrc/dsc_chain.hip,
+    YDBL_DSC3K_CHAIN=1) equals the four DSConv launches bit for bit, over several graph replays (the barrier
+    counters reset themselves), and no group barrier timed out."""
+    from ydbl.nn import modules as M
 
-    torch.manual_seed(cin + cout + h + 7)
-    x = torch.randn(n, cin, h, w)
-    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
-    b = torch.randn(cout)
-    ref = F.silu(F.conv2d(x.half().float(), wt.half().float(), b, 1, 1))
+    torch.manual_seed(n * 100 + h)
+    m = M.DSC3k(128, 128, n=2, e=1.0, k1=3, k2=7).eval()
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.weight.uniform_(0.5, 1.5), mod.bias.uniform_(-0.3, 0.3)
+                mod.running_mean.uniform_(-0.2, 0.2), mod.running_var.uniform_(0.5, 1.5)
+    x = torch.randn(n, 128, h, w)
     outs = []
-    for route in (ring, None):
-        if route is None:
-            monkeypatch.delenv("YDBL_HALO_RING", raising=False)
-        else:
-            monkeypatch.setenv("YDBL_HALO_RING", route)
+    for chain in ("0", "1", "2"):
+        monkeypatch.setenv("YDBL_DSC3K_CHAIN", chain)
         plan = _plan(torch.float16)
-        xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
-        ybuf = plan.alloc(n, h, w, cout + 8)
-        yv = ybuf.cslice(8, cout)
-        rv, mode = None, _lib.RES_NONE
-        if res:
-            r = torch.randn(n, cout, h, w, generator=torch.Generator().manual_seed(5))
-            rv = _tv_from_nchw(plan, r)
-            mode = _lib.RES_ADD
-        emit_dense(plan, xv, yv, wt, b, 1, 1, 1, _lib.ACT_SILU, rv, mode)
-        _run(plan)
-        outs.append(yv.nchw().float().cpu())
-        if res:
-            ref_r = r.half().float() + ref
-    torch.testing.assert_close(outs[0], ref_r if res else ref, rtol=3e-2, atol=3e-2)
-    if n * h * w >= 25600:  # (smaller maps take the block GEMM without the ring: no bitwise twin)
-        assert torch.equal(outs[0], outs[1])
+        xv = _tv_from_nchw(plan, x)
+        y = m.emit(plan, xv)
+        whats = [st.what for st in plan.steps]
+        assert ("DSC3k.chain" in whats) == (chain != "0"), whats
+        for _ in range(3):
+            plan.run()
+        torch.cuda.synchronize()
+        outs.append(y.nchw().float().cpu())
+        if chain != "0":
+            st = next(s for s in plan.steps if s.what == "DSC3k.chain")
+            sync = st.keep[-1]
+            assert int(sync.view(torch.int32).sum().item()) == 0  # counters reset, no time-out flag
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])

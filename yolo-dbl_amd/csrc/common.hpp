@@ -58,12 +58,23 @@ template <> struct HVec<float> {
 };
 
 // XCD-aware block order.  Workgroups are dealt round-robin over the 8 XCDs (block b runs on XCD
-// b % 8), each with its own L2; remapping so that XCD x walks the contiguous logical range
-// [x*n/8, (x+1)*n/8) keeps neighbouring tiles (shared halo rows, shared input tile of several
-// output-channel splits) in one L2.  Identity when n is not a multiple of 8.
+// b % 8), each with its own L2; remapping so that XCD x walks a contiguous logical range keeps
+// neighbouring tiles (shared halo rows, shared input tile of several output-channel splits) in one
+// L2.  Any n: XCD x receives the blocks x, x+8, ... (q + (x < r) of them for n = 8q + r) and takes
+// the logical range starting at x*q + min(x, r).
 __device__ __forceinline__ int xcd_remap(int b, int n) {
-  if (n & 7) return b;
-  return (b & 7) * (n >> 3) + (b >> 3);
+  const int x = b & 7, q = n >> 3, r = n & 7;
+  return x * q + min(x, r) + (b >> 3);
+}
+
+// (pixel tile, column block) of a 2-D conv grid (gridDim.x pixel tiles x gridDim.y column blocks) in XCD-aware
+// order: the logical order is pixel-major, column-minor, so the column blocks of one pixel tile and the
+// neighbouring pixel tiles (the 3x3 halo rows) share one L2 instead of being dealt to different XCDs.
+__device__ __forceinline__ void xcd_tile2(int& mb, int& nb) {
+  const int gy = gridDim.y;
+  const int f = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gy);  // dispatch order: x fastest
+  mb = f / gy;
+  nb = f - mb * gy;
 }
 
 // This lane's wave within the workgroup, as a scalar: hipcc's divergence analysis treats threadIdx.x >> 6 as

@@ -48,8 +48,10 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
   const int wm = wave % WM, wn = wave / WM;
-  const int m0 = blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
+  int mb, nb;
+  xcd_tile2(mb, nb);
+  const int m0 = mb * BM;
+  const int n0 = nb * BN;
 
   // ---- per-thread staging coordinates (vector v = tid + it*256: row v>>2, k-vector v&3)
   int64_t arow[A_IT];  // element offset of this thread's weight k-vector
@@ -219,7 +221,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
   __shared__ vec sw[NTN * 16 * WROW];
 
   const int tid = threadIdx.x;
-  int bid = blockIdx.x;
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tx = bid % tiles_x; bid /= tiles_x;
   const int ty = bid % tiles_y;
   const int b = bid / tiles_y;
@@ -371,7 +373,9 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int mb, nb;
+  xcd_tile2(mb, nb);
+  const int m0 = mb * BM, n0 = nb * BN;
   const int kv = tid & 15;  // every staging vector of this thread has k-vector kv
 
   int64_t arow[A_IT];  // element offset of this thread's weight k-vector
@@ -613,7 +617,6 @@ template <typename T, bool Q8>
 static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
   if constexpr (sizeof(T) == 2 && !Q8) {
     if (try_conv3x3_vw(a, kh, s)) return;
-    if (try_conv3x3_ring(a, kh, s)) return;
   }
   if (!Q8 && try_tile<T>(a, kh, s)) return;
   if (try_conv3x3_halo<T, Q8>(a, kh, s)) return;

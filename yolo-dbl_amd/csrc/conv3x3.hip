@@ -16,17 +16,14 @@
 // bank quads for any starting pixel, and the mixed-g lane groups of ds_read_b128
 // ({0-3,12-15,20-27}, ...) stay conflict-free; weights are [co/16][tap][g][co%16] for the same
 // reason.  Fused epilogue (bias, SiLU, residual add, channel-slice store) from conv_common.hpp.
-#include <stdlib.h>
-
 #include "conv_common.hpp"
 
 namespace ydbl {
 
 
-template <typename T, int S, int TH, int NTN, bool Q8, int KS = 1>
+template <typename T, int S, int TH, int NTN, bool Q8>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int tiles_x, int tiles_y,
-                                                              int co_splits, int diag = 0) {
-  // KS k-steps (of BK channels each) per chunk: one global round trip and two barriers per KS * BK channels
+                                                              int co_splits) {
   constexpr int TW = 16;
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;
@@ -38,8 +35,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   constexpr int TMW = (TH + 3) / 4;  // 16-pixel tiles (= output rows) per wave
   using vec = typename Vec<T>::type;
   using opv = typename Op<T, Q8>::lds;  // 8-byte e4m3 groups in fp8 mode (same slot layout)
-  __shared__ opv s_x[KS * XSLOTS];
-  __shared__ opv s_w[KS * WV];
+  __shared__ opv s_x[XSLOTS];
+  __shared__ opv s_w[WV];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -86,43 +83,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
   // raw loads, zero selects at the LDS store (vload_clamped): the next chunk stays in flight during the MFMAs
-  vec xr[KS][XIT];
-  opv wr[KS][WIT];
+  vec xr[XIT];
+  opv wr[WIT];
   bool cok = true;
-  // diag (timing-only experiment switch, wrong results): bit 0 = stage the weights of chunk 0 only, bit 1 = the
-  // halo of chunk 0 only, bit 2 = skip the MFMAs
-  const bool skip_w = diag & 1, skip_x = diag & 2;
-  bool first = true;
   auto load_chunk = [&](int c0) {
     cok = c0 < p.Cin;
 #pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      if (!(skip_x && !first)) {
+    for (int it = 0; it < XIT; ++it) xr[it] = vload_clamped(xsrc[it] + c0, p.x, xok[it] && cok);
 #pragma unroll
-        for (int it = 0; it < XIT; ++it) xr[k][it] = vload_clamped(xsrc[it] + c0 + k * BK, p.x, xok[it] && cok);
-      }
-      if (!(skip_w && !first)) {
-#pragma unroll
-        for (int it = 0; it < WIT; ++it) wr[k][it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0 + k * BK, wok[it] && cok);
-      }
-    }
+    for (int it = 0; it < WIT; ++it) wr[it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0, wok[it] && cok);
   };
   auto store_chunk = [&]() {
 #pragma unroll
-    for (int k = 0; k < KS; ++k) {
-      if (!(skip_x && !first)) {
+    for (int it = 0; it < XIT; ++it)
+      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
 #pragma unroll
-        for (int it = 0; it < XIT; ++it)
-          if (it * 256 + tid < XSLOTS)
-            s_x[k * XSLOTS + it * 256 + tid] = to_op<T, Q8>(vsel(xr[k][it], xok[it] && cok), p.qs);
-      }
-      if (!(skip_w && !first)) {
-#pragma unroll
-        for (int it = 0; it < WIT; ++it)
-          if (it * 256 + tid < WV) s_w[k * WV + it * 256 + tid] = vsel(wr[k][it], wok[it] && cok);
-      }
-    }
-    first = false;
+    for (int it = 0; it < WIT; ++it)
+      if (it * 256 + tid < WV) s_w[it * 256 + tid] = vsel(wr[it], wok[it] && cok);
   };
 
   f32x4 acc[NTN][TMW];
@@ -132,32 +109,31 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     for (int j = 0; j < TMW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one LDS buffer, refilled between barriers; the next chunk is in registers during the MFMAs (two buffers and
-  // one barrier per chunk measured even or slower: kbench bs16 384->64 @40^2 27.0 vs 26.7 us, 64->128 13.2 vs 15.7)
-  const int nchunks = p.Cin / (KS * BK);
+  // one barrier per chunk measured even or slower: kbench bs16 384->64 @40^2 27.0 vs 26.7 us, 64->128 13.2 vs 15.7;
+  // two k-steps per chunk, fewer barriers: 384->64 26.6 -> 28.2 us; timing split with the staging or the MFMAs
+  // switched off: staging holds 24.7 of 26.6 us; an LDS-DMA chunk ring (buffer_load ... lds, 2-4 chunks in flight,
+  // bit-identical) 26.4-27.1 us -- profiles/r05/r05_halo_*.txt)
+  const int nchunks = p.Cin / BK;
   load_chunk(0);
   store_chunk();
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
-    if (ch + 1 < nchunks) load_chunk((ch + 1) * KS * BK);  // (after chunk 0's store: `first` is false)
-    if (!(diag & 4))  // diag bit 2: no MFMAs (staging and barriers alone)
+    if (ch + 1 < nchunks) load_chunk((ch + 1) * BK);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap % 3;
+      opv af[NTN], bf[TMW];
 #pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        opv af[NTN], bf[TMW];
+      for (int i = 0; i < NTN; ++i) af[i] = s_w[((i * 9 + tap) * 4 + g) * 16 + r16];
 #pragma unroll
-        for (int i = 0; i < NTN; ++i) af[i] = s_w[k * WV + ((i * 9 + tap) * 4 + g) * 16 + r16];
-#pragma unroll
-        for (int j = 0; j < TMW; ++j) {
-          const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
-          bf[j] = s_x[k * XSLOTS + hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
-        }
-#pragma unroll
-        for (int j = 0; j < TMW; ++j)
-#pragma unroll
-          for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
+      for (int j = 0; j < TMW; ++j) {
+        const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
+        bf[j] = s_x[hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
       }
+#pragma unroll
+      for (int j = 0; j < TMW; ++j)
+#pragma unroll
+        for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
     }
     if (ch + 1 < nchunks) {
       __syncthreads();  // every wave is done reading this chunk
@@ -181,45 +157,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co);
 }
 
-template <typename T, bool Q8, int S, int TH, int KS = 1>
-static void launch_halo_ks(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0);
-
-// YDBL_HALO_KS=1|2: k-steps per staged chunk -- experiment switch
 template <typename T, bool Q8, int S, int TH>
-static void launch_halo(const ConvArgs<T>& a, hipStream_t s, int force_ntn = 0) {
-  constexpr int BK = 4 * Vec<T>::N;
-  const char* e = getenv("YDBL_HALO_KS");
-  if (e && atoi(e) == 2 && a.Cin % (2 * BK) == 0) launch_halo_ks<T, Q8, S, TH, 2>(a, s, force_ntn);
-  else launch_halo_ks<T, Q8, S, TH, 1>(a, s, force_ntn);
-}
-
-template <typename T, bool Q8, int S, int TH, int KS>
-static void launch_halo_ks(const ConvArgs<T>& a, hipStream_t s, int force_ntn) {
-  const char* de = getenv("YDBL_HALO_DIAG");  // timing-only experiment switch (wrong results): see the kernel
-  const int diag = de ? atoi(de) : 0;
+static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
   // most CUs with one workgroup; 32-channel slices double the grid (conv_bench.py bs16: 384->64 @40^2
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
-  // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench)
+  // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench;
+  // 16-channel slices and 4-row tiles lose on every head shape: profiles/r05/r05_halo_tile_ab.txt)
   constexpr int64_t n2_below = 512;
-  if (force_ntn == 1 || force_ntn == 2 || force_ntn == 4) {
-    const int cs = (int)cdiv(a.Cout, force_ntn * 16);
-    const unsigned grid = (unsigned)(ntiles * cs);
-    if (force_ntn == 1) conv3x3_halo_kernel<T, S, TH, 1, Q8, KS><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
-    else if (force_ntn == 2) conv3x3_halo_kernel<T, S, TH, 2, Q8, KS><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
-    else conv3x3_halo_kernel<T, S, TH, 4, Q8, KS><<<grid, 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
-    return;
-  }
   if (a.Cout <= 32) {
-    conv3x3_halo_kernel<T, S, TH, 2, Q8, KS><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1, diag);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {
     const int cs = (int)cdiv(a.Cout, 32);
-    conv3x3_halo_kernel<T, S, TH, 2, Q8, KS><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
+    conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   } else {
     const int cs = (int)cdiv(a.Cout, 64);
-    conv3x3_halo_kernel<T, S, TH, 4, Q8, KS><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs, diag);
+    conv3x3_halo_kernel<T, S, TH, 4, Q8><<<(unsigned)(ntiles * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
   }
 }
 
@@ -258,14 +213,6 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   (void)tiles8;
   // Cout <= 32 (one 32-channel slice: the weights are as many bytes per chunk as the halo): 16-row tiles from
   // 256 of them (DBL-n's 256->32 @80^2 at bs16, 400 tiles: 34.6 -> 31.8 us in graph, scripts/kbench.py)
-  // YDBL_HALO_TH=4|8|16 [YDBL_HALO_NTN=1|2|4]: experiment switch for tile-height / channel-slice A/Bs (kbench)
-  if (const char* e = getenv("YDBL_HALO_TH")) {
-    const char* f = getenv("YDBL_HALO_NTN");
-    const int th = atoi(e), ntn = f ? atoi(f) : 0;
-    if (th == 8) return launch_halo<T, Q8, 1, 8>(a, s, ntn), true;
-    if (th == 16) return launch_halo<T, Q8, 1, 16>(a, s, ntn), true;
-    if (th == 4) return launch_halo<T, Q8, 1, 4>(a, s, ntn), true;
-  }
   if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256)) launch_halo<T, Q8, 1, 16>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);
   return true;

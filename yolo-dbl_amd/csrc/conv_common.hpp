@@ -86,14 +86,12 @@ __device__ __forceinline__ typename Op<T, Q8>::lds load_wop(const T* w, int64_t 
 
 
 // LDS slot of halo pixel `pix` (row-major over the halo tile), k-vector g, in the halo kernels' "planar per 16-lane
-// run" layout (conv3x3.hip, conv3x3_ring.hip)
+// run" layout (conv3x3.hip)
 template <int S>
 __device__ __forceinline__ int hslot(int pix, int g) {
   return (pix / (16 * S)) * (64 * S) + g * (16 * S) + (pix % S) * 16 + ((pix / S) & 15);
 }
 
-// conv3x3_ring.hip: fp16 deep-K 3x3 stride 1 with an LDS-DMA chunk ring; false when not routed there.
-bool try_conv3x3_ring(const ConvArgs<_Float16>& a, int kh, hipStream_t s);
 // conv3x3.hip: halo-tiled 3x3 kernel for Cin >= 2 k-steps; false when the shape is not its own.
 template <typename T, bool Q8>
 bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s);

@@ -127,6 +127,7 @@ SIGNATURES = {
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_pair_nhwc": ([C.POINTER(DwConvDesc), C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dsconv_nhwc": ([C.POINTER(DsConvDesc), _P], C.c_int),
+    "ydbl_dsc3k_chain": ([C.POINTER(DsConvDesc), _P, _P, C.c_int32, _P], C.c_int),
     "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
     "ydbl_conv_stem": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _P, _P, C.c_int32, C.c_int32,
                         C.c_int32, _VP, _P], C.c_int),

@@ -683,10 +683,14 @@ class C3(PlanModule):
                     emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
                 mods = list(self.m)
                 t = buf.cslice(2 * c_, c_)
+                n0 = len(plan.steps)
                 for i, m in enumerate(mods[:-1]):
                     t = m.emit(plan, t, pre=pre if i == 0 else None)
-                return mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
-                                     pre=pre if len(mods) == 1 else None)
+                y = mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
+                                  pre=pre if len(mods) == 1 else None)
+                if os.environ.get("YDBL_DSC3K_CHAIN") in ("1", "2"):
+                    chain_dsc3k(plan, n0, xcd_local=os.environ["YDBL_DSC3K_CHAIN"] == "2")
+                return y
             emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
             emit_seq(plan, self.m, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
             return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
@@ -733,6 +737,26 @@ class C3(PlanModule):
                 and dw.bias is None and dw.in_channels == pw.out_channels == c_ and last.cv1.pw.out_channels == c_
                 and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.groups == 1
                 and c3.in_channels == 2 * c_ and c3.out_channels == c_ and isinstance(self.cv3.act, nn.SiLU))
+
+
+def chain_dsc3k(plan, n0: int, xcd_local: bool = False) -> bool:
+    """Experiment (YDBL_DSC3K_CHAIN=1, =2 for the XCD-local group barrier): replace the four DSConv launches plan.steps[n0:] of a DSC3k's two
+    DSBottlenecks (128 channels, k3 / k7, cv3 fused into the last) by one ydbl_dsc3k_chain launch (csrc/dsc_chain.hip,
+    per-image group barriers between the stages; bit-identical).  False (plan unchanged) when they are not that."""
+    steps = plan.steps[n0:]
+    if len(steps) != 4 or any(st.fn is not _lib.lib.ydbl_dsconv_nhwc for st in steps):
+        return False
+    descs = [st.args[0] for st in steps]
+    if [d.k for d in descs] != [3, 7, 3, 7] or any(d.x.c != 128 or d.y.c != 128 for d in descs):
+        return False
+    if descs[0].x.n * -(-descs[0].x.h // 8) * -(-descs[0].x.w // 8) > 160:
+        return False
+    arr = (_lib.DsConvDesc * 4)(*descs)
+    sync = plan.scratch(4 * (2 * descs[0].x.n + 1), zero=True)
+    keep = [k for st in steps for k in st.keep] + [arr, sync]
+    del plan.steps[n0:]
+    plan.launch("ydbl_dsc3k_chain", arr, sync.data_ptr(), None, int(xcd_local), what="DSC3k.chain", keep=keep)
+    return True
 
 
 class GhostBottleneck(PlanModule):
