@@ -558,8 +558,8 @@ def predict_main(args, model, world, rank, dev, half, fp8, dtype_name, cfg):
     el = timed_steps(step, args, world, lambda: torch.cuda.synchronize(dev), dev)
     if rank == 0:
         extra = {"dets_per_image": round(sum(len(r.boxes.data) for r in out["r"]) / B, 2),
-                 "via": "YOLO.predict(x, half=%s) per step (Results construction and one count sync included)"
-                        % half}
+                 "via": "YOLO.predict(x, half=%s) per step (Results construction included; the detections are read "
+                        "back when first accessed, after the timed steps)" % half}
         emit_line(args, world, el, dtype_name, cfg, extra, None, None)
     if world > 1:
         dist.destroy_process_group()

@@ -144,14 +144,6 @@ typedef struct {
   int32_t g0_act;
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
-/* Experiment (YDBL_DSC3K_CHAIN=1, ydbl.nn.modules.C3): DSC3k's two DSBottlenecks at 128 channels (block.py:1408-1503:
- * k3 DSConv, k7 DSConv + x, k3 DSConv, k7 DSConv + x with cv3 as the trailing GEMM) as ONE launch over 8x8 tiles, the
- * tiles of an image walking the four stages with a per-image group barrier between them; outputs bit-identical to
- * the four ydbl_dsconv_nhwc launches.  d: those four descriptors in order; at most 160 tiles in all.  sync: 2*N + 1
- * zeroed uint32 (left zeroed by the kernel; sync[2N] = 1 if a group barrier timed out).  stamps: NULL, or
- * [N * tiles][4 stages][start, done, barrier passed] uint64 s_memrealtime values (100 MHz).  xcd_local: group barriers
- * without L2 write-back / invalidate, relying on each image's tiles running on one XCD (used when N % 8 == 0). */
-int ydbl_dsc3k_chain(const ydbl_dsconv_desc* d, uint32_t* sync, uint64_t* stamps, int32_t xcd_local, void* stream);
 
 /* Depthwise convolution (groups = C), fp32 arithmetic.
  * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).
@@ -170,16 +162,40 @@ int ydbl_dwconv2d_nhwc(const ydbl_dwconv_desc* d, void* stream);
  * maps at 640), bit-identical to the two ydbl_dwconv2d_nhwc launches it falls back to otherwise. */
 int ydbl_dwconv2d_pair_nhwc(const ydbl_dwconv_desc* d0, const ydbl_dwconv_desc* d1, void* stream);
 
-/* NCHW fp32 image batch -> NHWC view (channels >= 3 zero-filled up to y.cs), optional scale (1/255). */
+/* Input binding: the batch a graph-captured plan reads, chosen when the plan RUNS (YOLO.predict on a device tensor
+ * without a staging copy).  When a kernel below gets a non-NULL `bind`, it takes the NCHW fp32 batch pointer from the
+ * device word *bind->x (16-byte aligned, the same shape as x) and the scale from the device scalar *bind->amax, the
+ * batch maximum, by LoadTensor's rule (U/data/loaders.py:561-566: x / 255 when max > 1 + FLT_EPSILON, else x; the
+ * division is the multiply by fp32(1/255) that the GPU division computes) -- instead of x and scale. */
+typedef struct {
+  const float* const* x; /* device word holding the batch pointer */
+  const float* amax;     /* device fp32 scalar: the batch maximum */
+} ydbl_input_bind;
+
+/* The batch maximum of an input binding, on the device (LoadTensor's /255 decision, U/data/loaders.py:561-566), in
+ * one launch: amax[0] = max of the n floats at x (16-byte aligned; NaN propagates as in torch.max) and, when scale
+ * is not NULL, scale[0] = fp32(1/255) if amax > 1 + FLT_EPSILON else 1.  work: ydbl_batch_max_work_ints() int32
+ * prepared by ydbl_batch_max_work_init (every call leaves them so); one work buffer per stream in flight. */
+int32_t ydbl_batch_max_work_ints(void);
+void ydbl_batch_max_work_init(int32_t* host_work);
+int ydbl_batch_max(const float* x, int64_t n, int32_t* work, float* amax, float* scale, void* stream);
+/* The same with the batch pointer read from the device word *xword when the launch runs (the first launch of a
+ * captured predict graph, include/ydbl.h ydbl_input_bind); the batch must be 16-byte aligned. */
+int ydbl_batch_max_bound(const float* const* xword, int64_t n, int32_t* work, float* amax, float* scale,
+                         void* stream);
+
+/* NCHW fp32 image batch -> NHWC view (channels >= 3 zero-filled up to y.cs), optional scale (1/255); bind: NULL or
+ * the input binding above. */
 int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,
-                            const ydbl_view* y, void* stream);
+                            const ydbl_view* y, const ydbl_input_bind* bind, void* stream);
 
 /* Stem: y = act(conv_kxk(x * scale) + bias) straight from an NCHW fp32 batch x [n][cin][h][w]
  * (cin = 3), w fp32 [cout][cin][k][k] (torch layout, BN folded), bias fp32 [cout]; y NHWC view with
  * y.c = cout (multiple of 4, <= 64); k = 3, pad = 1, stride 1 or 2.  In f16 mode the scaled input is rounded
  * to f16 before the conv (the reference's .half() input); arithmetic is fp32. */
 int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, float scale, const float* wt,
-                   const float* bias, int32_t k, int32_t stride, int32_t act, const ydbl_view* y, void* stream);
+                   const float* bias, int32_t k, int32_t stride, int32_t act, const ydbl_view* y,
+                   const ydbl_input_bind* bind, void* stream);
 
 /* y = a + gate * b (FullPAD_Tunnel). */
 int ydbl_gate_add(const ydbl_view* a, const ydbl_view* b, float gate, const ydbl_view* y, void* stream);
@@ -346,6 +362,7 @@ typedef struct {
   int32_t c0;
   const void* params;
   ydbl_view y;
+  ydbl_input_bind bind; /* {NULL, NULL}: read x / scale */
 } ydbl_stem2_desc;
 int64_t ydbl_conv_stem2_params_size(int32_t c0);
 int ydbl_conv_stem2_pack(const float* w0, const float* b0, const float* w1, const float* b1, int32_t c0, void* out);

@@ -43,7 +43,7 @@ for ci in sel:
     mid = plan.alloc(B, H, W, c0)
     wd, bd = w0.cuda(), b0.cuda()
     ms = mid.struct()
-    f_stem = lambda: _lib.lib.ydbl_conv_stem(x.data_ptr(), B, 3, H, W, 1.0, wd.data_ptr(), bd.data_ptr(), 3, 1, 1, ms, s)
+    f_stem = lambda: _lib.lib.ydbl_conv_stem(x.data_ptr(), B, 3, H, W, 1.0, wd.data_ptr(), bd.data_ptr(), 3, 1, 1, ms, None, s)
     p2 = Plan(torch.device("cuda"), torch.float16)
     emit_dense(p2, mid, y, w1, b1, 2, 1, 1, _lib.ACT_SILU)
     f_conv = lambda: p2.run()

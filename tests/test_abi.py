@@ -43,6 +43,7 @@ STRUCTS = {
     "ydbl_match_desc": "MatchDesc",
     "ydbl_letterbox_desc": "LetterboxDesc",
     "ydbl_stem2_desc": "Stem2Desc",
+    "ydbl_input_bind": "InputBind",
     "ydbl_bottleneck_desc": "BottleneckDesc",
     "ydbl_dysample_desc": "DySampleDesc",
     "ydbl_dysample2_desc": "DySample2Desc",

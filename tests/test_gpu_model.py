@@ -164,6 +164,67 @@ def test_predict_runs_benched_layout(golden_dir):
     assert len(list(p._sessions.values())[-1].children) == 0 and len(res3) == 3
 
 
+@pytest.mark.parametrize("batch,streams", [(5, 2), (3, 1)])
+def test_predict_reads_device_tensor_in_place(golden_dir, batch, streams):
+    """predict() on a contiguous fp32 device tensor binds the plans' input to it (include/ydbl.h ydbl_input_bind: no
+    staging copy; LoadTensor's /255 rule, U/data/loaders.py:561-566, applied by the stem kernels from the batch
+    maximum): detections bit-equal to the staging-copy path on the LoadTensor-scaled batch, for a [0, 1] and a
+    [0, 255] batch; the next plain session call goes back to the staging buffer; other tensors take the copy path."""
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    x01 = blob_images(batch, 160, seed=77).cuda()
+    got01 = None
+    for x, ref_in in ((x01, x01), (x01 * 255.0, x01 * 255.0 / 255.0)):
+        res = p.predict(x, half=True, conf=0.05, streams=streams)
+        s = list(p._sessions.values())[-1]
+        assert s._bound is x and len(s.children) == (streams if streams > 1 else 0)
+        got = [r.boxes.data.clone() for r in res]
+        d, c = s(ref_in)  # staging copy of the scaled batch: the binding is released
+        torch.cuda.synchronize()
+        assert s._bound is None
+        assert sum(len(g) for g in got) > 0
+        for i, g in enumerate(got):
+            assert torch.equal(g, d[i, : int(c[i])]), i
+        got01 = got01 or got
+    xs = torch.cat([x01, x01], 1)[:, :3]  # non-contiguous view: the copy path
+    assert not list(p._sessions.values())[-1].can_bind(xs)
+    res = p.predict(xs, half=True, conf=0.05, streams=streams)
+    assert list(p._sessions.values())[-1]._bound is None
+    for i, r in enumerate(res):
+        assert torch.equal(r.boxes.data, got01[i])
+
+
+def test_predict_back_to_back_calls_keep_their_batches(golden_dir):
+    """Back-to-back predict() calls on different device batches without a sync in between (the in-place path
+    alternates two binding slots on the session's own stream while the caller's stream runs ahead): every call's
+    Results hold its own batch's detections, bit-equal to a separate synchronous run of that batch, also when a
+    tensor is freed right after its call and its memory is reused."""
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    xs = [blob_images(8, 192, seed=s).cuda() for s in (11, 12, 13)]
+    xs[1] = xs[1] * 255.0  # this one takes LoadTensor's /255
+    ref = []
+    for x in xs:
+        r = p.predict(x, half=True, conf=0.05)
+        torch.cuda.synchronize()
+        ref.append([t.boxes.data.clone() for t in r])
+    outs = []
+    for rep in range(3):
+        for i, x in enumerate(xs):
+            outs.append((i, p.predict(x, half=True, conf=0.05)))
+        tmp = blob_images(8, 192, seed=99).cuda() * 3.0  # freed after its call: its memory goes back to the pool
+        outs.append((None, p.predict(tmp, half=True, conf=0.05)))
+        del tmp
+        junk = torch.full((8, 3, 192, 192), 7.0, device="cuda")  # may take tmp's memory
+        del junk
+    for i, res in outs:
+        if i is None:
+            continue
+        assert [torch.equal(t.boxes.data, r) for t, r in zip(res, ref[i])] == [True] * 8, i
+
+
 def _cpu_map50(o, x, labels, conf=0.001):
     """mAP@0.5 of the CPU oracle path under the same val protocol (multi-label NMS, conf .001)."""
     from oracle.ops import clip_boxes, non_max_suppression

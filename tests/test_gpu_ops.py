@@ -516,7 +516,7 @@ def test_stem(dtype, cout, s, h, w):
     yv = plan.alloc(n, ho, wo, cout)
     xd, wd, bd = x.to(DEV), wt.to(DEV), b.to(DEV)
     plan.launch("ydbl_conv_stem", xd.data_ptr(), n, 3, h, w, 1.0, wd.data_ptr(), bd.data_ptr(), 3, s,
-                _lib.ACT_SILU, yv.struct())
+                _lib.ACT_SILU, yv.struct(), None)
     _run(plan)
     tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **tol)
@@ -1227,35 +1227,34 @@ def test_lsk_fused_bit_identical(c, shape, sliced, monkeypatch):
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("n,h,w", [(16, 20, 20), (3, 20, 20), (8, 12, 20), (1, 8, 8)])
-def test_dsc3k_chain_bit_identical(monkeypatch, n, h, w):
-    """The DSC3k bottleneck pair at 128 channels as one launch with per-image group barriers (csrc/dsc_chain.hip,
-    YDBL_DSC3K_CHAIN=1) equals the four DSConv launches bit for bit, over several graph replays (the barrier
-    counters reset themselves), and no group barrier timed out."""
-    from ydbl.nn import modules as M
+@pytest.mark.parametrize("n", [1, 7, 4096, 3 * 160 * 160 * 5 + 3, 32 * 3 * 640 * 640])
+@pytest.mark.parametrize("kind", ["unit", "x255", "negative", "nan"])
+def test_batch_max(n, kind):
+    """ydbl_batch_max (predict()'s LoadTensor decision, U/data/loaders.py:561-566) against
+    torch.amax: the maximum bit for bit, NaN propagated, scale fp32(1/255) iff max > 1 + FLT_EPSILON."""
+    from ydbl import _lib
 
-    torch.manual_seed(n * 100 + h)
-    m = M.DSC3k(128, 128, n=2, e=1.0, k1=3, k2=7).eval()
-    with torch.no_grad():
-        for mod in m.modules():
-            if isinstance(mod, torch.nn.BatchNorm2d):
-                mod.weight.uniform_(0.5, 1.5), mod.bias.uniform_(-0.3, 0.3)
-                mod.running_mean.uniform_(-0.2, 0.2), mod.running_var.uniform_(0.5, 1.5)
-    x = torch.randn(n, 128, h, w)
-    outs = []
-    for chain in ("0", "1", "2"):
-        monkeypatch.setenv("YDBL_DSC3K_CHAIN", chain)
-        plan = _plan(torch.float16)
-        xv = _tv_from_nchw(plan, x)
-        y = m.emit(plan, xv)
-        whats = [st.what for st in plan.steps]
-        assert ("DSC3k.chain" in whats) == (chain != "0"), whats
-        for _ in range(3):
-            plan.run()
-        torch.cuda.synchronize()
-        outs.append(y.nchw().float().cpu())
-        if chain != "0":
-            st = next(s for s in plan.steps if s.what == "DSC3k.chain")
-            sync = st.keep[-1]
-            assert int(sync.view(torch.int32).sum().item()) == 0  # counters reset, no time-out flag
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(n, generator=g)
+    if kind == "x255":
+        x = x * 255.0
+    elif kind == "negative":
+        x = -x - 1.0
+    elif kind == "nan":
+        x[n // 2] = float("nan")
+    xd = x.to(DEV)
+    work = _lib.batch_max_work(DEV)
+    init = work.clone()
+    amax, scale = torch.empty(1, device=DEV), torch.empty(1, device=DEV)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):  # the work pair is left ready for the next call
+        _lib.check(_lib.lib.ydbl_batch_max(xd.data_ptr(), n, work.data_ptr(), amax.data_ptr(), scale.data_ptr(), st))
+    torch.cuda.synchronize()
+    assert torch.equal(work, init)
+    ref = torch.amax(x)
+    if kind == "nan":
+        assert torch.isnan(amax.cpu()[0]) and scale.item() == 1.0
+        return
+    assert amax.cpu()[0].item() == ref.item()
+    expect = torch.tensor(1.0 / 255.0, dtype=torch.float32).item() if ref.item() > 1.0 + 1.1920928955078125e-07 else 1.0
+    assert scale.item() == expect

@@ -77,6 +77,19 @@ __device__ __forceinline__ void xcd_tile2(int& mb, int& nb) {
   nb = f - mb * gy;
 }
 
+// Input binding (include/ydbl.h ydbl_input_bind): batch pointer and LoadTensor scale read when the kernel runs.
+struct InputBind {
+  const float* const* x;
+  const float* amax;
+};
+__device__ __forceinline__ const float* bound_x(const InputBind& ib, const float* x) { return ib.x ? *ib.x : x; }
+__device__ __forceinline__ float bound_scale(const InputBind& ib, float scale) {
+  return ib.x ? (*ib.amax > 1.0f + __FLT_EPSILON__ ? 1.0f / 255.0f : 1.0f) : scale;
+}
+__host__ inline InputBind input_bind(const ydbl_input_bind* b) {
+  return b ? InputBind{b->x, b->amax} : InputBind{nullptr, nullptr};
+}
+
 // This lane's wave within the workgroup, as a scalar: hipcc's divergence analysis treats threadIdx.x >> 6 as
 // per-lane, which puts every loop over a wave's share of the work (and its exec-mask bookkeeping) on the VALU.
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }

@@ -284,7 +284,9 @@ __global__ __launch_bounds__(NT) void dw_pair_kernel(DView<const T> x, DView<T> 
 // ------------------------------------------------------------------ input NCHW fp32 -> NHWC
 template <typename T>
 __global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x, int n, int c, int h, int w,
-                                                    float scale, DView<T> y) {
+                                                    float scale, DView<T> y, InputBind ib) {
+  x = bound_x(ib, x);
+  scale = bound_scale(ib, scale);
   const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t hw = (int64_t)h * w;
   if (pix >= (int64_t)n * hw) return;
@@ -592,16 +594,16 @@ extern "C" int ydbl_dwconv2d_pair_nhwc(const ydbl_dwconv_desc* d0, const ydbl_dw
 }
 
 extern "C" int ydbl_input_nchw_to_nhwc(const float* x, int32_t n, int32_t c, int32_t h, int32_t w, float scale,
-                                       const ydbl_view* y, void* stream) {
+                                       const ydbl_view* y, const ydbl_input_bind* bind, void* stream) {
   if (!x) return fail(YDBL_EINVAL, "input: null x");
   if (check_view(y, "input.y", true)) return YDBL_EINVAL;
   if (y->n != n || y->h != h || y->w != w || y->c < c) return fail(YDBL_EINVAL, "input: shape mismatch");
   hipStream_t s = as_stream(stream);
   const int64_t total = (int64_t)n * h * w;
   if (y->dtype == YDBL_F16)
-    input_kernel<_Float16><<<nblk(total), 256, 0, s>>>(x, n, c, h, w, scale, dview<_Float16>(*y));
+    input_kernel<_Float16><<<nblk(total), 256, 0, s>>>(x, n, c, h, w, scale, dview<_Float16>(*y), input_bind(bind));
   else
-    input_kernel<float><<<nblk(total), 256, 0, s>>>(x, n, c, h, w, scale, dview<float>(*y));
+    input_kernel<float><<<nblk(total), 256, 0, s>>>(x, n, c, h, w, scale, dview<float>(*y), input_bind(bind));
   return check_launch("ydbl_input_nchw_to_nhwc");
 }
 

@@ -24,7 +24,9 @@ template <> struct Rec<float> { using type = f32x4; };
 template <typename T, int NT, int S, bool V4>
 __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, int H, int W, float scale,
                                                    const float* __restrict__ wt, const float* __restrict__ bias,
-                                                   int act, DView<T> y) {
+                                                   int act, DView<T> y, InputBind ib) {
+  x = bound_x(ib, x);
+  scale = bound_scale(ib, scale);
   using rec = typename Rec<T>::type;
   constexpr bool F16 = sizeof(T) == 2;
   constexpr int KS = F16 ? 2 : 3;          // k-steps: 36 slots -> 2 x 32 (f16) / 3 x 16 (f32)
@@ -161,7 +163,8 @@ using namespace ydbl;
 
 extern "C" int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, float scale,
                               const float* wt, const float* bias, int32_t k, int32_t stride, int32_t act,
-                              const ydbl_view* y, void* stream) {
+                              const ydbl_view* y, const ydbl_input_bind* bind, void* stream) {
+  if (bind && (!bind->x || !bind->amax)) return fail(YDBL_EINVAL, "stem: input binding with a null pointer");
   if (!x || !wt || !bias) return fail(YDBL_EINVAL, "stem: null input/weights");
   if (check_view(y, "stem.y", true)) return YDBL_EINVAL;
   if (cin != 3) return fail(YDBL_EINVAL, "stem: cin must be 3 (RGB; K = 27 = one MFMA k-step)");
@@ -178,7 +181,7 @@ extern "C" int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h,
   const int nt = (cout + 15) / 16;
   const bool v4 = w % 4 == 0 && (reinterpret_cast<uintptr_t>(x) & 15) == 0;
   auto go = [&](auto kern, auto yv) {
-    kern<<<grid, 256, lds, s>>>(x, h, w, scale, wt, bias, act, yv);
+    kern<<<grid, 256, lds, s>>>(x, h, w, scale, wt, bias, act, yv, input_bind(bind));
     return check_launch("ydbl_conv_stem");
   };
 #define YDBL_STEM_CASE(T, NT)                                                                        \

@@ -103,7 +103,10 @@ __device__ unsigned long long g_st_stamps[8 * 16384];
 template <int C0, int TW, int TH, bool V4>
 __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__ x, int H, int W, float scale,
                                                        const unsigned char* __restrict__ params,
-                                                       DView<_Float16> y, int tiles_x, int tiles_y, int nblocks) {
+                                                       DView<_Float16> y, int tiles_x, int tiles_y, int nblocks,
+                                                       InputBind ib) {
+  x = bound_x(ib, x);
+  scale = bound_scale(ib, scale);
   using Cfg = Stem2Cfg<C0, TW, TH>;
   const h8* w0f = reinterpret_cast<const h8*>(params);
   const h8* w1f = w0f + Cfg::W0F;
@@ -372,6 +375,7 @@ extern "C" int ydbl_conv_stem2_pack(const float* w0, const float* b0, const floa
 extern "C" int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream) {
   if (!d) return fail(YDBL_EINVAL, "stem2: null descriptor");
   if (!d->x || !d->params) return fail(YDBL_EINVAL, "stem2: null input/parameters");
+  if (!d->bind.x != !d->bind.amax) return fail(YDBL_EINVAL, "stem2: input binding with a null pointer");
   if (check_view(&d->y, "stem2.y", true)) return YDBL_EINVAL;
   if (d->y.dtype != YDBL_F16) return fail(YDBL_EINVAL, "stem2: fp16 activations only");
   if (d->cin != 3) return fail(YDBL_EINVAL, "stem2: cin must be 3");
@@ -386,7 +390,7 @@ extern "C" int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream) {
     const int64_t nb = (int64_t)tiles_x * tiles_y * d->n;
     if (nb > 0x7fffffff) return fail(YDBL_EINVAL, "stem2: grid too large");
     kern<<<(unsigned)nb, 256, lds, s>>>(d->x, d->h, d->w, d->scale, reinterpret_cast<const unsigned char*>(d->params),
-                                        dview<_Float16>(d->y), tiles_x, tiles_y, (int)nb);
+                                        dview<_Float16>(d->y), tiles_x, tiles_y, (int)nb, input_bind(&d->bind));
     return check_launch("ydbl_conv_stem2");
   };
   const bool v4 = d->w % 4 == 0 && (reinterpret_cast<uintptr_t>(d->x) & 15) == 0;

@@ -81,9 +81,14 @@ class NmsDesc(C.Structure):
                 ("count_stride", C.c_int64)]
 
 
+class InputBind(C.Structure):
+    """ydbl_input_bind: device word holding the batch pointer, device fp32 batch maximum (LoadTensor's /255 rule)."""
+    _fields_ = [("x", C.c_void_p), ("amax", C.c_void_p)]
+
+
 class Stem2Desc(C.Structure):
     _fields_ = [("x", C.c_void_p), ("n", C.c_int32), ("cin", C.c_int32), ("h", C.c_int32), ("w", C.c_int32),
-                ("scale", C.c_float), ("c0", C.c_int32), ("params", C.c_void_p), ("y", View)]
+                ("scale", C.c_float), ("c0", C.c_int32), ("params", C.c_void_p), ("y", View), ("bind", InputBind)]
 
 
 class DySampleDesc(C.Structure):
@@ -127,10 +132,14 @@ SIGNATURES = {
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_pair_nhwc": ([C.POINTER(DwConvDesc), C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dsconv_nhwc": ([C.POINTER(DsConvDesc), _P], C.c_int),
-    "ydbl_dsc3k_chain": ([C.POINTER(DsConvDesc), _P, _P, C.c_int32, _P], C.c_int),
-    "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP, _P], C.c_int),
+    "ydbl_batch_max_work_ints": ([], C.c_int32),
+    "ydbl_batch_max_work_init": ([_P], None),
+    "ydbl_batch_max": ([_P, C.c_int64, _P, _P, _P, _P], C.c_int),
+    "ydbl_batch_max_bound": ([_P, C.c_int64, _P, _P, _P, _P], C.c_int),
+    "ydbl_input_nchw_to_nhwc": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _VP,
+                                 C.POINTER(InputBind), _P], C.c_int),
     "ydbl_conv_stem": ([_P, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_float, _P, _P, C.c_int32, C.c_int32,
-                        C.c_int32, _VP, _P], C.c_int),
+                        C.c_int32, _VP, C.POINTER(InputBind), _P], C.c_int),
     "ydbl_gate_add": ([_VP, _VP, C.c_float, _VP, _P], C.c_int),
     "ydbl_pool_up_concat": ([_VP, _VP, _VP, _VP, _P], C.c_int),
     "ydbl_dysample": ([_VP, _VP, C.c_int32, _VP, _P], C.c_int),
@@ -204,3 +213,12 @@ def dtype_code(dt: torch.dtype) -> int:
 
 def version() -> str:
     return lib.ydbl_version().decode()
+
+
+def batch_max_work(device) -> "torch.Tensor":
+    """A ready work buffer for ydbl_batch_max on `device` (include/ydbl.h)."""
+    import torch
+
+    host = torch.empty(int(lib.ydbl_batch_max_work_ints()), dtype=torch.int32)
+    lib.ydbl_batch_max_work_init(host.data_ptr())
+    return host.to(device)

@@ -95,9 +95,24 @@ class _LazyHWC:
 
     def __getitem__(self, i):
         if self.hwc is None:
-            x = self.im.float() if self.scale is None else self.im * self.scale
+            scale = self.scale() if callable(self.scale) else self.scale
+            x = self.im.float() if scale is None else self.im * scale
             self.hwc = x.permute(0, 2, 3, 1)
         return self.hwc[i]
+
+
+class _LazyCounts:
+    """The per-image detection counts of a batch, read to the host once, on first access: predict() returns without
+    waiting for the GPU, and the batch's Results synchronise when one of them is first looked at.  cnt: the device
+    tensor, or a callable producing it then (a session slot's outputs, copied out on first access)."""
+
+    def __init__(self, cnt):
+        self.cnt, self.host = cnt, None
+
+    def __getitem__(self, i):
+        if self.host is None:
+            self.host = (self.cnt() if callable(self.cnt) else self.cnt).tolist()
+        return self.host[i]
 
 
 class Model:
@@ -263,36 +278,52 @@ class Model:
                 return self._predict_frames(frames, args, dev, t0, stream, paths)
             raise TypeError(f"unsupported source type {type(source).__name__}")
         im = check_tensor_source(source, int(self.model.stride.max()))
-        scale = None
-        if im.device == dev:
-            # LoadTensor's /255 rule on the tensor's device without a host sync: the session's input copy multiplies
-            # by fp32(1/255) when max > 1 (torch's GPU x / 255.0 is exactly that product), by 1 otherwise
-            one, inv = _scale_consts(dev)
-            scale = torch.where(im.amax() > 1.0 + (torch.finfo(im.dtype).eps if im.is_floating_point() else 0.0),
-                                inv, one)
-        else:  # host tensors are scaled on the host, where the reference's LoadTensor does it, then moved
+        if im.device != dev:  # host tensors are scaled on the host, where the reference's LoadTensor does it, then moved
             im = load_tensor_source(im).to(dev, non_blocking=True).float()
         b, _, h, w = im.shape
-        s = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
-                         agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
-                         streams=args["streams"], fp8_calibration=args["fp8_calibration"])
+        kw = dict(half=args["half"], conf=args["conf"], iou=args["iou"], max_det=args["max_det"],
+                  agnostic=args["agnostic_nms"], classes=args["classes"], device=dev, fp8=args["fp8"],
+                  streams=args["streams"], fp8_calibration=args["fp8_calibration"])
+        s = self.session(b, h, w, **kw)
         t1 = time.perf_counter()
-        det, cnt = s(im, scale)
+        one, inv = _scale_consts(dev)
+        thr = 1.0 + (torch.finfo(im.dtype).eps if im.is_floating_point() else 0.0)
+        bo = None
+        if s.can_bind(im):
+            # read in place: the plans' input binding points at im, and the stem kernels apply LoadTensor's /255
+            # rule from its device-side maximum (no staging copy, no host sync, no per-call copy of the outputs;
+            # DetectSession.launch_bound)
+            bo = s.launch_bound(im)
+        else:
+            # LoadTensor's /255 rule on the device without a host sync: the input copy multiplies by fp32(1/255)
+            # when max > 1 (torch's GPU x / 255.0 is exactly that product), by 1 otherwise
+            scale = torch.where(im.amax() > thr, inv, one)
+            det, cnt = s(im, scale)
         if self._stale(s):  # weights edited since the session was compiled: rebuild and run again
-            det, cnt = self.session(b, h, w, half=args["half"], conf=args["conf"], iou=args["iou"],
-                                    max_det=args["max_det"], agnostic=args["agnostic_nms"], classes=args["classes"],
-                                    device=dev, fp8=args["fp8"], streams=args["streams"],
-                                    fp8_calibration=args["fp8_calibration"])(im, scale)
-        counts = cnt.tolist()  # one sync per batch
+            s = self.session(b, h, w, **kw)
+            scale = torch.where(im.amax() > thr, inv, one)
+            (det, cnt), bo = s(im, scale), None
+        # no host sync here: each image's boxes are a view of the batch's det, cut at its count when first accessed
+        # (_LazyCounts: one sync for the batch) -- on the copy path one device copy of det | count made now (the
+        # session's buffers are reused by the next call); orig_img a view of the input batch (HWC, as LoadTensor
+        # hands it over), made on first access.  speed["inference"] is the launch time.
+        if bo is not None:  # the slot's outputs, copied out of the slot on first access (or when it is reused)
+            dets, counts, scale = None, _LazyCounts(lambda: bo.detach().count), (lambda: bo.detach().scale[0])
+        elif getattr(s, "out_flat", None) is not None:  # det | count: one copy
+            flat = s.out_flat.clone()
+            dets, counts = flat[: det.numel()].view(det.shape), _LazyCounts(flat[det.numel():].view(torch.int32))
+        else:
+            dets, counts = det.clone(), _LazyCounts(cnt.clone())
         t2 = time.perf_counter()
         speed = {"preprocess": (t1 - t0) * 1e3 / b, "inference": (t2 - t1) * 1e3 / b, "postprocess": 0.0}
-        # one copy of the batch's detections (the session's buffers are reused by the next call); each image's
-        # boxes are a view of it, and orig_img a view of the input batch (HWC, as LoadTensor hands it over)
-        dets = det[:, : max(counts, default=0)].clone()
-        hwc = _LazyHWC(im, scale)  # orig_img: the LoadTensor-scaled image, HWC, computed on first access
+        hwc = _LazyHWC(im, scale)
         names, shape = self.model.names, (h, w)
+        if bo is not None:
+            box = lambda i: bo.detach().det[i, : counts[i]]  # noqa: E731
+        else:
+            box = lambda i: dets[i, : counts[i]]  # noqa: E731
         results = [Results(lambda i=i: hwc[i], path=f"image{i}.jpg", names=names, speed=speed, orig_shape=shape,
-                           boxes=lambda i=i, c=c: dets[i, :c]) for i, c in enumerate(counts)]
+                           boxes=lambda i=i: box(i)) for i in range(b)]
         return iter(results) if stream else results
 
     def _predict_frames(self, frames, args, dev, t0, stream, paths=None):

@@ -10,6 +10,7 @@ layout used by the multi-GPU path.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import torch
 
@@ -28,6 +29,45 @@ def default_streams(batch: int) -> int:
     return 2 if batch >= SPLIT_MIN_BATCH else 1
 
 
+class BoundOutputs:
+    """A predict() call's outputs in a session's binding slot (DetectSession.launch_bound): det [B, max_det, 6],
+    count [B] and LoadTensor's scale, valid as views of the slot until detach() copies them out (on first access, or
+    when the slot comes round again while this object is alive)."""
+
+    def __init__(self, det, count, flat, scale):
+        self.det, self.count, self.flat, self.scale, self.own = det, count, flat, scale, False
+
+    def detach(self):
+        if not self.own:
+            flat = self.flat.clone()
+            n = self.det.numel()
+            self.det, self.count = flat[:n].view(self.det.shape), flat[n:].view(torch.int32)
+            self.flat, self.scale, self.own = flat, self.scale.clone(), True
+        return self
+
+
+class _EagerSlot:
+    """use_graph=False: a binding slot's launches run eagerly (the descriptors are pointed at the slot per run)."""
+
+    def __init__(self, session, k, pre):
+        self.s, self.k, self.pre = session, k, pre
+
+    def replay(self):
+        det, count, _, _ = self.s._pout[self.k]
+        self.s._set_slot(self.k, det, count)
+        self.pre.run()
+        for p in self.s.plans:
+            p.run()
+        self.s._set_slot(0)
+
+
+def _det_count(batch: int, max_det: int, dev):
+    """det [B, max_det, 6] fp32 and count [B] int32 as views of ONE zeroed buffer (flat), so a caller keeping a batch's
+    outputs past the next launch copies them in one go (predict())."""
+    flat = torch.zeros(batch * max_det * 6 + batch, dtype=torch.float32, device=dev)
+    return flat[: batch * max_det * 6].view(batch, max_det, 6), flat[batch * max_det * 6:].view(torch.int32), flat
+
+
 class DetectSession:
     """streams = k > 1: the batch is split into k contiguous sub-batches, each compiled into its own launch
     plan (own buffers) writing into slices of the shared det / count (/ pred) outputs; the k plans are captured
@@ -39,7 +79,7 @@ class DetectSession:
     def __init__(self, model, batch: int, h: int, w: int, dtype=torch.float16, conf=0.25, iou=0.7, max_det=300,
                  multi_label=False, agnostic=False, classes=None, max_nms=30000, max_wh=7680, clip=True,
                  keep_pred=False, use_graph=True, device="cuda", fp8=False, streams=1, gather_rows=None, nms=True,
-                 fp8_calibration=None, _outputs=None):
+                 fp8_calibration=None, _outputs=None, _bind=None):
         if fp8 and dtype != torch.float16:
             raise ValueError("fp8 operands run on the fp16 activation path (half=True)")
         self.model, self.batch, self.h, self.w, self.dtype = model, batch, h, w, dtype
@@ -51,6 +91,12 @@ class DetectSession:
         self.conf, self.iou, self.max_det = float(conf), float(iou), int(max_det)
         self.children = []
         self.records = None
+        # predict()'s in-place path (launch_bound): binding slot 0 is the session's own staging buffer (load()), slots
+        # 1 and 2 alternate between predict() calls, each with its own graph (LoadTensor maximum + the plans) and its
+        # own det | count outputs, kept until the slot comes round again (then copied if its Results still live)
+        self._bound = None  # the last tensor launch_bound() read (introspection)
+        self._calls, self._slot_ptrs, self._pgraph, self._pout, self._pheld = 0, {}, {}, {}, {}
+        self._max_work = None
         if _outputs is None and gather_rows is not None:
             # one record per image [det (max_det*6 fp32) | count (int32) | pad]: the boxes and counts of a batch-
             # sharded predict leave the GPU in ONE all-gather (ydbl.parallel); rows >= batch stay empty padding
@@ -69,7 +115,11 @@ class DetectSession:
             self._init_split(model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes, max_nms,
                              max_wh, clip, keep_pred, use_graph, device, fp8, streams, nms, _outputs)
             return
-        cm = model.compile(batch, h, w, dtype, device=device)
+        if _bind is None:  # a top-level session owns the binding slots (a split session's children get views)
+            self.bind_ptrs = torch.empty((3, 1), dtype=torch.int64, device=torch.device(device))
+            self.bind_amax = torch.zeros((3, 1), dtype=torch.float32, device=torch.device(device))
+            _bind = (self.bind_ptrs[0], self.bind_amax[0])
+        cm = model.compile(batch, h, w, dtype, device=device, bind=_bind)
         self.compiled = cm
         plan: Plan = cm.plan
         det = cm.detect
@@ -84,12 +134,12 @@ class DetectSession:
         self.cand_cls = torch.empty((batch, cap), dtype=torch.int32, device=dev)
         self.cand_idx = torch.empty((batch, cap), dtype=torch.int32, device=dev)
         self.cand_count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+        self.out_flat = None
         if _outputs is not None:  # slices of a split session's shared outputs
             self.det, self.count, self.pred = _outputs
         else:
             self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
-            self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
-            self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+            self.det, self.count, self.out_flat = _det_count(batch, self.max_det, dev)
         self.classes_t = (torch.tensor(list(classes), dtype=torch.int32, device=dev) if classes is not None else None)
         ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(batch, cap, max_nms)), dtype=torch.uint8, device=dev)
         plan.buffers += [self.cand_box, self.cand_score, self.cand_cls, self.cand_idx, self.cand_count, self.det,
@@ -115,6 +165,8 @@ class DetectSession:
         self.plans = [plan]
         self.use_graph = use_graph
         self._graph = None
+        if hasattr(self, "bind_ptrs"):
+            self._init_slots()
 
     def _init_split(self, model, batch, h, w, dtype, conf, iou, max_det, multi_label, agnostic, classes, max_nms,
                     max_wh, clip, keep_pred, use_graph, device, fp8, streams, nms, outputs):
@@ -124,24 +176,29 @@ class DetectSession:
         det = model.model[-1]
         nc = det.nc
         A = sum((h // int(s)) * (w // int(s)) for s in det.stride.tolist())
+        self.out_flat = None
         if outputs is not None:
             self.det, self.count, self.pred = outputs
         else:
-            self.det = torch.zeros((batch, self.max_det, 6), dtype=torch.float32, device=dev)
-            self.count = torch.zeros((batch,), dtype=torch.int32, device=dev)
+            self.det, self.count, self.out_flat = _det_count(batch, self.max_det, dev)
             self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
         self.bounds = [shard_bounds(batch, streams, r) for r in range(streams)]
-        for a, b in self.bounds:
+        # per binding slot: one batch-pointer word per sub-batch plan, one batch maximum for all (launch_bound())
+        self.bind_ptrs = torch.empty((3, streams), dtype=torch.int64, device=dev)
+        self.bind_amax = torch.zeros((3, 1), dtype=torch.float32, device=dev)
+        for i, (a, b) in enumerate(self.bounds):
             outs = (self.det[a:b], self.count[a:b], self.pred[a:b] if keep_pred else None)
             self.children.append(DetectSession(model, b - a, h, w, dtype, conf, iou, max_det, multi_label, agnostic,
                                                classes, max_nms, max_wh, clip, keep_pred, use_graph, device, fp8,
-                                               nms=nms, _outputs=outs))
+                                               nms=nms, _outputs=outs,
+                                               _bind=(self.bind_ptrs[0, i:i + 1], self.bind_amax[0])))
         self.streams = [torch.cuda.Stream(dev) for _ in self.children]
         self.plans = [c.plan for c in self.children]
         self.plan = self.plans[0]
         self.use_graph = use_graph
         self._graph = None  # all sub-batch plans as branches of one hipGraph (runtime.BranchGraphRunner)
         self.nc, self.A = self.children[0].nc, self.children[0].A
+        self._init_slots()
 
     @property
     def cand_count(self):
@@ -154,10 +211,92 @@ class DetectSession:
         self._cand_count = v
 
     # ------------------------------------------------------------------ execution
+    def _own_inputs(self):
+        return [c.compiled.input.data_ptr() for c in (self.children or [self])]
+
+    def can_bind(self, x: torch.Tensor) -> bool:
+        """launch_bound() takes x: a contiguous fp32 tensor of the session's shape on its device, every sub-batch 16-byte
+        aligned (the stem kernels' vector loads)."""
+        if (not isinstance(x, torch.Tensor) or x.dtype != torch.float32 or x.device != self.det.device
+                or not x.is_contiguous() or tuple(x.shape) != (self.batch, 3, self.h, self.w)
+                or (self.fp8 and not self.fp8_ready)):  # (an uncalibrated fp8 session calibrates on a loaded batch)
+            return False
+        per = 3 * self.h * self.w * 4
+        return all((x.data_ptr() + a * per) % 16 == 0 for a, _ in (self.bounds if self.children else [(0, 0)]))
+
+    def _owners(self):
+        return [c.compiled for c in self.children] if self.children else [self.compiled]
+
+    def _nms_descs(self):
+        return [st.args[0] for c in (self.children or [self]) for st in c.plan.steps if st.fn.__name__ == "ydbl_nms"]
+
+    def _init_slots(self):
+        own = torch.tensor(self._own_inputs(), dtype=torch.int64)
+        self.bind_ptrs.copy_(own.expand(self.bind_ptrs.shape[0], -1))
+
+    def _set_slot(self, k: int, det: torch.Tensor | None = None, count: torch.Tensor | None = None):
+        """Point the plans' input-reading launches at binding slot k and their NMS outputs at det / count (default:
+        the session's own), before a capture; the C-ABI copies both into the kernel arguments at launch."""
+        for i, cm in enumerate(self._owners()):
+            cm.set_bind(self.bind_ptrs[k, i:i + 1], self.bind_amax[k])
+        det = self.det if det is None else det
+        count = self.count if count is None else count
+        for nd, (a, b) in zip(self._nms_descs(), self.bounds if self.children else [(0, self.batch)]):
+            nd.out, nd.out_count = det[a:b].data_ptr(), count[a:b].data_ptr()
+
+    def launch_bound(self, x: torch.Tensor) -> "BoundOutputs":
+        """predict()'s path for a device batch: the plans read x in place (include/ydbl.h ydbl_input_bind) -- no
+        staging copy -- and apply LoadTensor's /255 rule (U/data/loaders.py:561-566) from x's maximum, which the
+        launch computes on the device first (ydbl_batch_max_bound, the first node of the same graph: no host sync).
+        Calls alternate between two binding slots, each with its own captured graph and its own det | count
+        outputs, so nothing is copied per call: the outputs stay in the slot until it comes round again, and are
+        copied then only if the call's BoundOutputs (its Results) are still alive -- or on first access."""
+        if not self.can_bind(x):
+            raise ValueError("launch_bound(): a contiguous fp32 batch of the session's shape on its device, 16-byte "
+                             "aligned")
+        k = 1 + self._calls % 2
+        self._calls += 1
+        dev = x.device
+        held = self._pheld.get(k)
+        held = held() if held is not None else None
+        if held is not None:
+            held.detach()  # a live result of the call two back: copy it out of the slot before the slot is rewritten
+        per = 3 * self.h * self.w * 4
+        ptrs = [x.data_ptr() + a * per for a, _ in (self.bounds if self.children else [(0, 0)])]
+        if ptrs != self._slot_ptrs.get(k):  # (the words keep their value from call to call for the same tensor)
+            self.bind_ptrs[k].copy_(torch.tensor(ptrs, dtype=torch.int64), non_blocking=True)
+            self._slot_ptrs[k] = ptrs
+        g = self._pgraph.get(k)
+        if g is None:
+            if self.fp8 and not self.fp8_ready:
+                self.calibrate_fp8(calibration=self.fp8_calibration)
+            if self._max_work is None:
+                self._max_work = _lib.batch_max_work(dev)
+            det, count, flat = _det_count(self.batch, self.max_det, dev)
+            scale = torch.empty(1, dtype=torch.float32, device=dev)
+            self._pout[k] = (det, count, flat, scale)
+            pre = Plan(dev, self.dtype)
+            pre.launch("ydbl_batch_max_bound", self.bind_ptrs[k, 0:1].data_ptr(), x.numel(), self._max_work.data_ptr(),
+                       self.bind_amax[k].data_ptr(), scale.data_ptr(), what="LoadTensor.max")
+            self._set_slot(k, det, count)
+            if self.use_graph:
+                g = (BranchGraphRunner(self.plans, pre=pre) if self.children else GraphRunner(self.plan, pre=pre))
+            else:
+                g = _EagerSlot(self, k, pre)
+            self._set_slot(0)
+            self._pgraph[k] = g
+        g.replay()
+        det, count, flat, scale = self._pout[k]
+        out = BoundOutputs(det, count, flat, scale)
+        self._pheld[k] = weakref.ref(out)
+        self._bound = x
+        return out
+
     def load(self, x: torch.Tensor, scale: torch.Tensor | None = None):
         """Copy a BCHW batch into the static input buffer (LoadTensor semantics are the caller's); scale: a 0-dim
-        fp32 device tensor the batch is multiplied by on the way in (predict()'s /255 decision, taken on the device:
-        x * fp32(1/255) is what torch's GPU division by 255.0 computes, so no host sync is needed for it)."""
+        fp32 device tensor the batch is multiplied by on the way in (x * fp32(1/255) is what torch's GPU division by
+        255.0 computes, so no host sync is needed for it)."""
+        self._bound = None
         if self.children:
             if tuple(x.shape[1:]) != (3, self.h, self.w) or x.shape[0] != self.batch:
                 raise ValueError(f"input shape {tuple(x.shape)} != session shape {(self.batch, 3, self.h, self.w)}")
@@ -201,6 +340,7 @@ class DetectSession:
             c._graph = None  # descriptors changed: recapture
             c.fp8_ready = True
         self._graph = None
+        self._pgraph.clear()
         self.fp8_ready = True
         return n
 

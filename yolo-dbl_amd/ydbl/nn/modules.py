@@ -257,8 +257,9 @@ def stem_ok(m, ch: int) -> bool:
             and c.out_channels % 4 == 0 and c.out_channels <= 64 and isinstance(m.act, (nn.SiLU, nn.Identity)))
 
 
-def emit_stem(m: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: int, w: int) -> TV:
-    """preprocess (U/engine/predictor.py:116-134) + first Conv (conv.py:39-63, BN folded) in one kernel."""
+def emit_stem(m: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: int, w: int, bind=None) -> TV:
+    """preprocess (U/engine/predictor.py:116-134) + first Conv (conv.py:39-63, BN folded) in one kernel.
+    bind: an _lib.InputBind (the batch pointer / LoadTensor maximum read when the plan runs) or None."""
     wf, bf = m.folded()
     s = m.conv.stride[0]
     ho, wo = conv_out_hw(h, w, 3, s, 1, 1)
@@ -266,7 +267,7 @@ def emit_stem(m: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: i
     wd = plan.const(wf.float().contiguous())
     bd = plan.const((bf if bf is not None else torch.zeros(m.conv.out_channels)).float())
     plan.launch("ydbl_conv_stem", x_nchw.data_ptr(), n, ch, h, w, 1.0, wd.data_ptr(), bd.data_ptr(), 3, s,
-                _act_code(m.act), y.struct(), what="Stem.conv3x3", keep=[wd, bd])
+                _act_code(m.act), y.struct(), bind, what="Stem.conv3x3", keep=[wd, bd, bind])
     return y
 
 
@@ -282,8 +283,9 @@ def stem2_ok(m0, m1, ch: int, dtype) -> bool:
 
 
 def emit_stem2(m0: "Conv", m1: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int, ch: int, h: int, w: int,
-               out: TV | None = None) -> TV:
-    """preprocess + layers 0 and 1 (conv.py:39-63, BN folded) in one kernel; layer 0's map stays in LDS."""
+               out: TV | None = None, bind=None) -> TV:
+    """preprocess + layers 0 and 1 (conv.py:39-63, BN folded) in one kernel; layer 0's map stays in LDS.
+    bind: an _lib.InputBind or None (emit_stem)."""
     w0, b0 = m0.folded()
     w1, b1 = m1.folded()
     c0 = m0.conv.out_channels
@@ -295,7 +297,8 @@ def emit_stem2(m0: "Conv", m1: "Conv", plan: Plan, x_nchw: torch.Tensor, n: int,
     args = [t.float().contiguous() for t in (w0, b0, w1, b1)]
     _lib.check(_lib.lib.ydbl_conv_stem2_pack(*[t.data_ptr() for t in args], c0, host.data_ptr()), "ydbl_conv_stem2_pack")
     params = plan.const(host)
-    d = _lib.Stem2Desc(x_nchw.data_ptr(), n, ch, h, w, 1.0, c0, params.data_ptr(), y.struct())
+    d = _lib.Stem2Desc(x_nchw.data_ptr(), n, ch, h, w, 1.0, c0, params.data_ptr(), y.struct(),
+                       bind if bind is not None else _lib.InputBind())
     plan.launch("ydbl_conv_stem2", d, what="Stem.conv3x3x2", keep=[params, d])
     return y
 
@@ -683,14 +686,10 @@ class C3(PlanModule):
                     emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
                 mods = list(self.m)
                 t = buf.cslice(2 * c_, c_)
-                n0 = len(plan.steps)
                 for i, m in enumerate(mods[:-1]):
                     t = m.emit(plan, t, pre=pre if i == 0 else None)
-                y = mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
-                                  pre=pre if len(mods) == 1 else None)
-                if os.environ.get("YDBL_DSC3K_CHAIN") in ("1", "2"):
-                    chain_dsc3k(plan, n0, xcd_local=os.environ["YDBL_DSC3K_CHAIN"] == "2")
-                return y
+                return mods[-1].emit(plan, t, buf.cslice(0, c_), cv3=(self.cv3, buf.cslice(c_, c_), out),
+                                     pre=pre if len(mods) == 1 else None)
             emit_merged(plan, [self.cv2, self.cv1], x, buf.cslice(c_, 2 * c_))
             emit_seq(plan, self.m, buf.cslice(2 * c_, c_), buf.cslice(0, c_))
             return self.cv3.emit(plan, buf.cslice(0, 2 * c_), out)
@@ -737,26 +736,6 @@ class C3(PlanModule):
                 and dw.bias is None and dw.in_channels == pw.out_channels == c_ and last.cv1.pw.out_channels == c_
                 and c3.kernel_size == (1, 1) and c3.stride == (1, 1) and c3.groups == 1
                 and c3.in_channels == 2 * c_ and c3.out_channels == c_ and isinstance(self.cv3.act, nn.SiLU))
-
-
-def chain_dsc3k(plan, n0: int, xcd_local: bool = False) -> bool:
-    """Experiment (YDBL_DSC3K_CHAIN=1, =2 for the XCD-local group barrier): replace the four DSConv launches plan.steps[n0:] of a DSC3k's two
-    DSBottlenecks (128 channels, k3 / k7, cv3 fused into the last) by one ydbl_dsc3k_chain launch (csrc/dsc_chain.hip,
-    per-image group barriers between the stages; bit-identical).  False (plan unchanged) when they are not that."""
-    steps = plan.steps[n0:]
-    if len(steps) != 4 or any(st.fn is not _lib.lib.ydbl_dsconv_nhwc for st in steps):
-        return False
-    descs = [st.args[0] for st in steps]
-    if [d.k for d in descs] != [3, 7, 3, 7] or any(d.x.c != 128 or d.y.c != 128 for d in descs):
-        return False
-    if descs[0].x.n * -(-descs[0].x.h // 8) * -(-descs[0].x.w // 8) > 160:
-        return False
-    arr = (_lib.DsConvDesc * 4)(*descs)
-    sync = plan.scratch(4 * (2 * descs[0].x.n + 1), zero=True)
-    keep = [k for st in steps for k in st.keep] + [arr, sync]
-    del plan.steps[n0:]
-    plan.launch("ydbl_dsc3k_chain", arr, sync.data_ptr(), None, int(xcd_local), what="DSC3k.chain", keep=keep)
-    return True
 
 
 class GhostBottleneck(PlanModule):

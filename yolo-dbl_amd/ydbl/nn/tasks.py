@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from ..runtime import TV, Plan, round_up, weights_signature, ydbl_env  # noqa: F401 (re-exported)
+from .. import _lib
 from . import modules as M
 
 CFG_DIR = Path(__file__).resolve().parent.parent / "cfg" / "models"
@@ -267,12 +268,23 @@ class DetectionModel(nn.Module):
     def is_fused(self):
         return self._fused
 
-    def compile(self, batch: int, h: int, w: int, dtype=torch.float16, device="cuda") -> "CompiledModel":
-        """Build the launch plan of one forward: input NCHW fp32 [batch,3,h,w] -> per-level head outputs."""
+    def compile(self, batch: int, h: int, w: int, dtype=torch.float16, device="cuda", bind=None) -> "CompiledModel":
+        """Build the launch plan of one forward: input NCHW fp32 [batch,3,h,w] -> per-level head outputs.
+        The plan reads its batch through an input binding (include/ydbl.h ydbl_input_bind): bind_ptr, a device int64
+        holding the batch pointer (initially the plan's own staging buffer ``input``), and bind_amax, a device fp32
+        batch maximum for LoadTensor's /255 rule (0: scale 1).  bind = (bind_ptr, bind_amax) shares them with a
+        caller (a split session: one word per sub-batch plan, one maximum)."""
         plan = Plan(torch.device(device), dtype)
         inp = plan.alloc(batch, h, w, 8)  # RGB padded to 8 channels (16-byte vectors)
         x_nchw = torch.empty((batch, self.yaml["ch"], h, w), dtype=torch.float32, device=plan.device)
         plan.buffers.append(x_nchw)
+        if bind is None:
+            bind = (torch.empty(1, dtype=torch.int64, device=plan.device),
+                    torch.zeros(1, dtype=torch.float32, device=plan.device))
+        bind_ptr, bind_amax = bind
+        bind_ptr.fill_(x_nchw.data_ptr())
+        plan.buffers += [bind_ptr, bind_amax]
+        ib = _lib.InputBind(bind_ptr.data_ptr(), bind_amax.data_ptr())
         # Concat outputs are allocated up front; their producers write straight into the slices.
         layers = list(self.model)
         shapes = _propagate_shapes(layers, batch, h, w, self.yaml["ch"])
@@ -300,7 +312,7 @@ class DetectionModel(nn.Module):
                  and M.stem2_ok(layers[0], layers[1], self.yaml["ch"], dtype))
         if stem is None:
             plan.launch("ydbl_input_nchw_to_nhwc", x_nchw.data_ptr(), batch, self.yaml["ch"], h, w, 1.0, inp.struct(),
-                        what="input")
+                        ib, what="input", keep=[ib])
         for m in layers:
             plan.cur_layer = m.i  # (ydbl.quant names fp8 candidates by the layer that emitted them)
             if stem2 and m is layers[1]:
@@ -308,11 +320,11 @@ class DetectionModel(nn.Module):
                 continue
             if m is stem and stem2:  # preprocess + layers 0 and 1 in one kernel
                 x = M.emit_stem2(layers[0], layers[1], plan, x_nchw, batch, self.yaml["ch"], h, w,
-                                 cat_buf.get(1, out_hint.get(1)))
+                                 cat_buf.get(1, out_hint.get(1)), bind=ib)
                 y.append(None)  # layer 0's map is never materialised
                 continue
             if m is stem:  # preprocess + first Conv fused, straight from the NCHW batch
-                x = M.emit_stem(m, plan, x_nchw, batch, self.yaml["ch"], h, w)
+                x = M.emit_stem(m, plan, x_nchw, batch, self.yaml["ch"], h, w, bind=ib)
                 y.append(x)
                 continue
             if m.f != -1:
@@ -320,11 +332,18 @@ class DetectionModel(nn.Module):
             out = cat_buf.get(m.i, out_hint.get(m.i))
             x = M.emit_module(m, plan, x, out)
             y.append(x)
-        return CompiledModel(plan, x_nchw, inp, x, self.model[-1])
+        cm = CompiledModel(plan, x_nchw, inp, x, self.model[-1])
+        cm.bind_ptr, cm.bind_amax = bind_ptr, bind_amax
+        # the InputBind records the launches read (retargeted by CompiledModel.set_bind)
+        cm.bind_holders = [st.args[0].bind if st.fn.__name__ == "ydbl_conv_stem2" else st.args[-1]
+                           for st in plan.steps if st.fn.__name__ in ("ydbl_conv_stem2", "ydbl_conv_stem",
+                                                                       "ydbl_input_nchw_to_nhwc")]
+        return cm
 
 
 class CompiledModel:
-    """A compiled forward: ``input`` (NCHW fp32 staging buffer) -> ``levels`` (per-level NHWC head outputs)."""
+    """A compiled forward: ``input`` (NCHW fp32 staging buffer) -> ``levels`` (per-level NHWC head outputs);
+    bind_ptr / bind_amax: its input binding (DetectionModel.compile)."""
 
     def __init__(self, plan: Plan, x_nchw: torch.Tensor, inp: TV, levels: list[TV], detect: M.Detect):
         self.plan, self.input, self.inp, self.levels, self.detect = plan, x_nchw, inp, levels, detect
@@ -332,6 +351,12 @@ class CompiledModel:
     def feats(self):
         """Reference-layout per-level outputs x[i] = cat(box, cls) as NCHW views (no copy)."""
         return [lv.nchw() for lv in self.levels]
+
+    def set_bind(self, ptr: torch.Tensor, amax: torch.Tensor):
+        """Point every input-reading launch at another binding (device int64 batch-pointer word, fp32 maximum); the
+        C-ABI copies the record into the kernel arguments at launch, so a graph captured afterwards keeps it."""
+        for h in self.bind_holders:
+            h.x, h.amax = ptr.data_ptr(), amax.data_ptr()
 
 
 def _propagate_shapes(layers, batch, h, w, ch):

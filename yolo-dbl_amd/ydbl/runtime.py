@@ -25,7 +25,7 @@ from ._lib import View, lib
 # The YDBL_* switches that change what a plan builds or launches (plan-builder fusions in ydbl.nn.modules / tasks,
 # routing in the C-ABI, read at build or at each launch).  tests/test_host_api.py checks this list against the
 # names the sources read.
-SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_DSC3K_CHAIN", "YDBL_HG_UNFUSED",
+SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_HG_UNFUSED",
             "YDBL_LSK_UNFUSED", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_NO_BNECK", "YDBL_NO_CV1_FUSE",
             "YDBL_NO_CV3_FUSE", "YDBL_NO_FUSE_PAD", "YDBL_NO_MERGE", "YDBL_NO_STEM2")
 
@@ -275,17 +275,21 @@ class Plan:
 class GraphRunner:
     """Captures Plan.run into a hipGraph (torch.cuda.CUDAGraph is hipGraph on ROCm) and replays it."""
 
-    def __init__(self, plan: Plan, warmup: int = 1):
+    def __init__(self, plan: Plan, warmup: int = 1, pre: Plan | None = None):
         self.plan = plan
         side = torch.cuda.Stream(plan.device)
         side.wait_stream(torch.cuda.current_stream(plan.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):
+                if pre is not None:
+                    pre.run(side.cuda_stream)
                 plan.run(side.cuda_stream)
         torch.cuda.current_stream(plan.device).wait_stream(side)
         torch.cuda.synchronize(plan.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
+            if pre is not None:
+                pre.run()
             plan.run()
         torch.cuda.synchronize(plan.device)
 
@@ -299,7 +303,8 @@ class BranchGraphRunner:
     graph per plan, each replayed on its own stream: DBL-n bs32 fp16 1.88-1.89 vs 1.93-1.94 ms per step
     (scripts/graph_branch_probe.py)."""
 
-    def __init__(self, plans, warmup: int = 1):
+    def __init__(self, plans, warmup: int = 1, pre: Plan | None = None):
+        """pre: a plan run before the fork (both branches wait for it)."""
         for p in plans:
             p.check_single_stream()
         dev = plans[0].device
@@ -307,6 +312,8 @@ class BranchGraphRunner:
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(side):
             for _ in range(warmup):
+                if pre is not None:
+                    pre.run(side.cuda_stream)
                 for p in plans:
                     p.run(side.cuda_stream)
         torch.cuda.current_stream(dev).wait_stream(side)
@@ -315,6 +322,8 @@ class BranchGraphRunner:
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             cap = torch.cuda.current_stream(dev)
+            if pre is not None:
+                pre.run()
             for st in self.sides:
                 st.wait_stream(cap)
             plans[0].run()
