@@ -2,6 +2,7 @@
 spread does not enter the comparison.  Each variant is a separate session (the session key holds the knobs).
 
     python scripts/ab_bench.py "A:" "B:YDBL_NO_CV3_FUSE=1;YDBL_NO_MERGE=1" [--model n] [--batch 32] [--streams 2] [--rounds 5]
+    python scripts/ab_bench.py "S2:" "S3:STREAMS=3" "S4:STREAMS=4"        (sub-batch graphs per variant)
 """
 import argparse
 import os
@@ -46,11 +47,12 @@ def main():
     sess = {}
     for spec in a.variants:
         name, env = parse(spec)
+        streams = int(env.pop("STREAMS", a.streams))  # "S3:STREAMS=3": sub-batch graphs of this variant
         for k in [k for k in os.environ if k.startswith("YDBL_")]:
             del os.environ[k]
         os.environ.update(base)
         os.environ.update(env)
-        s = model.session(a.batch, a.imgsz, a.imgsz, half=True, conf=0.25, iou=0.7, streams=a.streams)
+        s = model.session(a.batch, a.imgsz, a.imgsz, half=True, conf=0.25, iou=0.7, streams=streams)
         s.load(x)
         for _ in range(5):
             s()
