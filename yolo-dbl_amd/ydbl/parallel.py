@@ -42,7 +42,13 @@ def record_views(records: torch.Tensor, max_det: int) -> tuple[torch.Tensor, tor
 
 
 def gather_records(records: torch.Tensor, out: torch.Tensor, group=None) -> torch.Tensor:
-    """The path's one collective: every rank's [b_max, width] records into out [world * b_max, width]."""
+    """The path's one collective: every rank's [b_max, width] records into out [world * b_max, width].  On a gloo
+    group with device tensors (ranks sharing a GPU, e.g. the world-2 GPU test) the records go through host memory."""
+    if records.is_cuda and dist.get_backend(group) == "gloo":
+        host = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(host, records.cpu(), group=group)
+        out.copy_(host)
+        return out
     dist.all_gather_into_tensor(out, records, group=group)
     return out
 
