@@ -52,6 +52,9 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   xcd_tile2(mb, nb);
   const int m0 = mb * BM;
   const int n0 = nb * BN;
+  __shared__ __align__(16) float s_bias[BN];
+  BiasStage<BN> bst;
+  bst.fetch(p.bias, n0, p.Cout);
 
   // ---- per-thread staging coordinates (vector v = tid + it*256: row v>>2, k-vector v&3)
   int64_t arow[A_IT];  // element offset of this thread's weight k-vector
@@ -152,6 +155,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
 #pragma unroll
   for (int u = 0; u < PF; ++u) load_step(u, ra[u], aok[u], rb[u], rok[u]);
   store_step(0, ra[0], aok[0], rb[0], rok[0]);
+  bst.commit(s_bias);
   __syncthreads();
   // The loads are unconditional (past the end they are masked no-ops), so the waitcnt pass sees one fixed
   // order of outstanding loads and waits only for the slot being stored.
@@ -189,7 +193,7 @@ __global__ __launch_bounds__(256) void conv_igemm_kernel(ConvArgs<T> p) {
   }
 #pragma unroll
   for (int i = 0; i < TN; ++i) co[i] = n0 + wn * TN * 16 + i * 16 + 4 * g;
-  conv_epilogue<T, TN, TM, Q8>(p, acc, pp, pv, co);
+  conv_epilogue<T, TN, TM, Q8>(p, acc, pp, pv, co, s_bias, n0);
 }
 
 // Spatial-tile 3x3 conv for thin inputs (Cin <= 32, the high-resolution backbone layers).
@@ -227,6 +231,9 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
   const int b = bid / tiles_y;
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - p.PAD, ix0 = ox0 * S - p.PAD;
+  __shared__ __align__(16) float s_bias[NTN * 16];
+  BiasStage<NTN * 16> bst;
+  bst.fetch(p.bias, 0, p.Cout);
   {  // stage the input tile (loads batched 4 deep before their LDS stores)
     constexpr int TOT = IH * IW * CV;
     for (int base = 0; base < TOT; base += 4 * 256) {
@@ -261,6 +268,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
       }
     }
   }
+  bst.commit(s_bias);
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6;
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(256) void conv3x3_tile_kernel(ConvArgs<T> p, int ti
   }
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = i * 16 + 4 * g;
-  conv_epilogue<T, NTN, TM>(p, acc, pp, pv, co);
+  conv_epilogue<T, NTN, TM>(p, acc, pp, pv, co, s_bias, 0);
 }
 
 template <typename T, int CIN, int S, int TH, int TW, int NTN>
@@ -376,7 +384,8 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   int mb, nb;
   xcd_tile2(mb, nb);
   const int m0 = mb * BM, n0 = nb * BN;
-  const int kv = tid & 15;  // every staging vector of this thread has k-vector kv
+  const int kv = tid & 15;
+  // (no LDS-staged bias here: the extra bytes cost a workgroup per CU at 80 KB of staging)  // every staging vector of this thread has k-vector kv
 
   int64_t arow[A_IT];  // element offset of this thread's weight k-vector
   bool aval[A_IT];

@@ -51,6 +51,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const int co0 = cs * NTN * 16;
+  __shared__ __align__(16) float s_bias[NTN * 16];
+  BiasStage<NTN * 16> bst;
+  bst.fetch(p.bias, co0, p.Cout);
 
   // Staging walks LDS slots linearly (consecutive lanes -> consecutive 16-byte slots, so the
   // ds_write_b128s are conflict-free) and gathers the matching global vectors: a wave still
@@ -116,6 +119,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   const int nchunks = p.Cin / BK;
   load_chunk(0);
   store_chunk();
+  bst.commit(s_bias);
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
     if (ch + 1 < nchunks) load_chunk((ch + 1) * BK);
@@ -154,7 +158,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   int co[NTN];
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
-  conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co);
+  conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co, s_bias, co0);
 }
 
 template <typename T, bool Q8, int S, int TH>
@@ -244,6 +248,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_vw_kernel(ConvArgs<_Float16> p
   int t = xcd_remap(blockIdx.x, ntiles * co_splits);
   const int cs = t % co_splits;  // output-channel slice of NWG * TPW * 16 channels
   t /= co_splits;
+  __shared__ __align__(16) float s_bias[NWG * TPW * 16];
+  BiasStage<NWG * TPW * 16> bst;
+  bst.fetch(p.bias, cs * NWG * TPW * 16, p.Cout);
   const int tx = t % tiles_x, ty = (t / tiles_x) % tiles_y, img = t / (tiles_x * tiles_y);
   const int oy0 = ty * TH, ox0 = tx * TW;
 
@@ -280,6 +287,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_vw_kernel(ConvArgs<_Float16> p
 #pragma unroll
   for (int tt = 0; tt < TPW; ++tt) co[tt] = (cg * TPW + tt) * 16 + 4 * g;
   const unsigned char* in_b = s_in + (g * PIN + r16) * 16;
+  bst.commit(s_bias);
   __syncthreads();
 
   // 2. rows j0, j0+1 of the tile per pass; B for (row j, column r16, tap) at record (j+dy)*IP + r16+dx
@@ -311,7 +319,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_vw_kernel(ConvArgs<_Float16> p
       pv[r] = oy < p.Ho && ox < p.Wo;
       pp[r] = ((int64_t)img * p.Ho + oy) * p.Wo + ox;
     }
-    conv_epilogue<_Float16, TPW, ROWS, false>(p, acc, pp, pv, co);
+    conv_epilogue<_Float16, TPW, ROWS, false>(p, acc, pp, pv, co, s_bias, cs * NWG * TPW * 16);
   }
 }
 

@@ -127,17 +127,43 @@ __device__ __forceinline__ f32x4 mfma_op(const typename Op<T, Q8>::lds& a, const
   else return mfma_chunk<T>(a, b, c);
 }
 
+// The workgroup's N output channels' bias from c0 on, for the epilogue to read from LDS (conv_epilogue's sb):
+// read from global memory after the k-loop, the bias cost every launch one more dependent round trip at its very
+// end.  fetch() issues the loads at the start of the first round trip, commit() stores them into LDS just before
+// that round trip's barrier (a store right after its load would wait on every load issued before it).  256-thread
+// workgroups; clamped like the epilogue's own loads.
+template <int N>
+struct BiasStage {
+  static constexpr int IT = (N + 255) / 256;
+  float v[IT];
+  __device__ __forceinline__ void fetch(const float* bias, int c0, int cout) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) v[it] = bias ? bias[min(c0 + (int)threadIdx.x + it * 256, cout - 1)] : 0.f;
+  }
+  __device__ __forceinline__ void commit(float* s) const {
+#pragma unroll
+    for (int it = 0; it < IT; ++it)
+      if ((int)threadIdx.x + it * 256 < N) s[threadIdx.x + it * 256] = v[it];
+  }
+};
+
 // Epilogue of one wave's TN x TM accumulator tiles: lane owns output channels co[i]..co[i]+3 of
 // pixel pp[j].  Every load is unconditional from a clamped address (bias once; the residual of a
 // pixel for all TN tiles at once) so the loads overlap; only the stores are predicated.
+// sb: the bias staged in LDS for channels sb0.. (16-byte aligned), or nullptr to load it here.
 template <typename T, int TN, int TM, bool Q8 = false>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs<T>& p, const f32x4 (&acc)[TN][TM],
-                                              const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN]) {
+                                              const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN],
+                                              const float* sb = nullptr, int sb0 = 0) {
   const bool c4 = (p.Cout & 3) == 0;  // uniform: co..co+3 in range whenever co < Cout
   float bv[TN][4];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
-    if (p.bias) {
+    if (sb) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(sb + co[i] - sb0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = b4[q];
+    } else if (p.bias) {
       if (c4) {
         load_f<4>(p.bias + min(co[i], p.Cout - 4), bv[i]);
       } else {
@@ -253,17 +279,30 @@ __device__ __forceinline__ void conv_tail_1x1(const ConvArgs<T>& p, const f32x4 
 
 // The same tail from the values the epilogue stored (ys = y rounded to T, per lane [TN][TM][4]): no activation
 // recomputed.  Lanes of one pixel share pv, so the xor-shuffles only mix lanes of the same pixel.
+// s_t: the weights [4][Cout] staged in LDS (rows past nt3 zero), or nullptr to read them from global memory (a
+// late round trip of 16 x nt3 scalar loads per lane at the very end of the launch: kbench pair 64+tail @80^2 bs16 24.8 vs 20.5 us, profiles/r05/r05_bias_lds_ab.txt).
 template <typename T, int TN, int TM>
 __device__ __forceinline__ void conv_tail_1x1_vals(const ConvArgs<T>& p, const float (&ys)[TN][TM][4],
                                                    const int64_t (&pp)[TM], const bool (&pv)[TM], const int (&co)[TN],
-                                                   int g) {
+                                                   int g, const float* s_t = nullptr) {
   float wv[TN][4][4];
+  if (s_t) {
 #pragma unroll
-  for (int i = 0; i < TN; ++i)
+    for (int i = 0; i < TN; ++i)
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
+      for (int k = 0; k < 4; ++k) {
+        const f32x4 w4 = *reinterpret_cast<const f32x4*>(s_t + k * p.Cout + co[i]);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) wv[i][q][k] = k < p.nt3 ? p.t3w[k * p.Cout + co[i] + q] : 0.f;
+        for (int q = 0; q < 4; ++q) wv[i][q][k] = w4[q];
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TN; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wv[i][q][k] = k < p.nt3 ? p.t3w[k * p.Cout + co[i] + q] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < TM; ++j) {
     float part[4] = {0.f, 0.f, 0.f, 0.f};

@@ -27,7 +27,7 @@ template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG = false, 
 __global__ __launch_bounds__(NT, 1) void dsc_lean_kernel(ConvArgs<_Float16> p, const float* __restrict__ dww,
                                                           const float* __restrict__ dwb, int dw_act, int tiles_x,
                                                           int tiles_y, int ntiles) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LeanLds<C, CO, K, S, TH, TW, NT, TG, PRE>::BYTES];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LeanLds<C, CO, K, S, TH, TW, NT, TG, PRE, TAIL>::BYTES];
   lean_tile<C, CO, K, S, TH, TW, NT, TG, TAIL, PRE>(p, dww, dwb, dw_act, xcd_remap(blockIdx.x, ntiles), tiles_x,
                                                           tiles_y, smem);
 }

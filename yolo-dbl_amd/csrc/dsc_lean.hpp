@@ -7,7 +7,7 @@ namespace ydbl {
 __device__ __forceinline__ int lean_bswz(int row, int kv) { return row * 4 + (kv ^ (((row >> 2) & 1) << 1)); }
 
 // LDS carve-up of one lean tile
-template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool PRE>
+template <int C, int CO, int K, int S, int TH, int TW, int NT, bool TG, bool PRE, bool TAIL = false>
 struct LeanLds {
   static constexpr int IH = (TH - 1) * S + K, IW = (TW - 1) * S + K, IWP = IW | 1, NQ = C / 4;
   static constexpr int NPX = TH * TW, NKS = C / 32, PNP = PRE ? (IH * IW + 15) / 16 * 16 : 16;
@@ -15,7 +15,10 @@ struct LeanLds {
   static constexpr int W = (X + IH * IWP * NQ * 8 + 15) / 16 * 16;          // f32x4 [K * K * NQ]
   static constexpr int B = W + K * K * NQ * 16;                             // h8 [NKS * NPX * 4]
   static constexpr int P = B + NKS * NPX * 4 * 16;                          // h8 [2 * PNP * 4] (PRE)
-  static constexpr int BYTES = P + (PRE ? 2 * PNP * 4 * 16 : 16);
+  static constexpr int T = P + (PRE ? 2 * PNP * 4 * 16 : 16);               // f32 [4][CO] class-conv weights (TAIL)
+  static constexpr int BI = T + (TAIL ? 4 * CO * 4 : 0);                    // f32 [CO] pointwise bias
+  static constexpr int BI2 = BI + CO * 4;                                   // f32 [CO] trailing-GEMM bias (TG)
+  static constexpr int BYTES = BI2 + (TG ? CO * 4 : 0);
 };
 
 // One TH x TW output tile (linear tile index `tile`: image-major, then tile row, tile column).
@@ -58,7 +61,7 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
   // are this DSConv's input; B tile [2 k-steps][halo pixel, padded to 16][slot], one 16-channel tile pair per wave
   static_assert(!PRE || (C == 64 && CO == 64 && S == 1 && !TG && !TAIL && WAVES == 4), "leading 1x1 layout");
   constexpr int PNP = PRE ? (IH * IW + 15) / 16 * 16 : 16, PNT = PNP / 16;
-  using L = LeanLds<C, CO, K, S, TH, TW, NT, TG, PRE>;
+  using L = LeanLds<C, CO, K, S, TH, TW, NT, TG, PRE, TAIL>;
   h4* s_x = reinterpret_cast<h4*>(smem + L::X);      // fp16 halo, [row][col][quad]
   f32x4* s_w = reinterpret_cast<f32x4*>(smem + L::W);  // fp32 taps (rounded to fp16), [tap][quad]
   h8* s_b = reinterpret_cast<h8*>(smem + L::B);      // pointwise B tile, [k-step][pixel][slot]
@@ -119,6 +122,23 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
 #pragma unroll
     for (int e = 0; e < 4; ++e) wr[it][e] = float(T(w[e]));  // the reference's .half() weights
   }
+  // the pointwise bias (+ TG's g2b, + TAIL's class-conv weights [k][CO]) for LDS: loaded here, in the first round
+  // trip, and stored just before its barrier (a store right after its load waits on every load issued before it).
+  // Read from global after the MFMAs they cost one more round trip at the very end; kept in VGPRs from the start
+  // they cost 16 registers and a wave per SIMD.
+  constexpr int BIT = (CO + NT - 1) / NT, TLT = TAIL ? (4 * CO + NT - 1) / NT : 0;
+  float bir[BIT], b2r[TG ? BIT : 1], tlr[TLT > 0 ? TLT : 1];
+#pragma unroll
+  for (int it = 0; it < BIT; ++it) {
+    const int i = min(tid + it * NT, CO - 1);
+    bir[it] = p.bias[i];
+    if constexpr (TG) b2r[it] = p.g2b[i];
+  }
+#pragma unroll
+  for (int it = 0; it < TLT; ++it) {
+    const int i = min(tid + it * NT, 4 * CO - 1);
+    tlr[it] = i / CO < p.nt3 ? p.t3w[i] : 0.f;
+  }
   h8 af[TN][NKS];
 #pragma unroll
   for (int i = 0; i < TN; ++i) {
@@ -126,6 +146,7 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
 #pragma unroll
     for (int m = 0; m < NKS; ++m) af[i][m] = vload(p.w + (int64_t)row * p.KPAD + m * 32 + g * 8);
   }
+
   // PRE: tile i = 0 of this wave = 16 channels of the cv1 half (C + 16 wave.., over the whole halo, before the
   // depthwise), i = 1 = 16 channels of the cv2 half (16 wave.., over the output pixels only, after the pointwise)
   h8 a0[2][2];
@@ -143,7 +164,6 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
 #pragma unroll
   for (int it = 0; it < TIT; ++it)
     if (tid + it * NT < TAPV) s_w[tid + it * NT] = wr[it];
-
   {
     int64_t pp[TM];
     bool pv[TM];
@@ -192,6 +212,15 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
         s_p[(cv >> 2) * PNP * 4 + lean_bswz(px, cv & 3)] = h8{0, 0, 0, 0, 0, 0, 0, 0};
       }
     }
+#pragma unroll
+    for (int it = 0; it < BIT; ++it)
+      if (tid + it * NT < CO) {
+        reinterpret_cast<float*>(smem + L::BI)[tid + it * NT] = bir[it];
+        if constexpr (TG) reinterpret_cast<float*>(smem + L::BI2)[tid + it * NT] = b2r[it];
+      }
+#pragma unroll
+    for (int it = 0; it < TLT; ++it)
+      if (tid + it * NT < 4 * CO) reinterpret_cast<float*>(smem + L::T)[tid + it * NT] = tlr[it];
     __syncthreads();
     if constexpr (PRE) {
       // ---- 1b. leading 1x1 over the halo on MFMA (k-steps in channel order, epilogue as conv_epilogue's):
@@ -286,7 +315,11 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
       }
     float bv[TN][4];
 #pragma unroll
-    for (int i = 0; i < TN; ++i) load_f<4>(p.bias + co[i], bv[i]);
+    for (int i = 0; i < TN; ++i) {
+      const f32x4 b4 = *reinterpret_cast<const f32x4*>(smem + L::BI + co[i] * 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bv[i][q] = b4[q];
+    }
     float ys[TAIL ? TN : 1][TAIL ? TM : 1][4];  // TAIL: the stored y values for the class conv
 #pragma unroll
     for (int j = 0; j < TM; ++j) {
@@ -337,7 +370,7 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
       }
     }
     if constexpr (TAIL && NCG == 1 && TN == 4 && !TG) {  // Detect class conv over the 64 output channels (CO == 64)
-      conv_tail_1x1_vals<T, TN, TM>(p, ys, pp, pv, co, g);
+      conv_tail_1x1_vals<T, TN, TM>(p, ys, pp, pv, co, g, reinterpret_cast<const float*>(smem + L::T));
     }
     if constexpr (TG) {
       // ---- 4. trailing GEMM: g2y = act(W2 [y ; g2x] + b2), K = 2*CO in channel order (the unfused cv3's k-steps)
@@ -358,7 +391,11 @@ __device__ __forceinline__ void lean_tile(const ConvArgs<_Float16>& p, const flo
       }
       float b2v[TN][4];
 #pragma unroll
-      for (int i = 0; i < TN; ++i) load_f<4>(p.g2b + co[i], b2v[i]);
+      for (int i = 0; i < TN; ++i) {
+        const f32x4 b4 = *reinterpret_cast<const f32x4*>(smem + L::BI2 + co[i] * 4);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b2v[i][q] = b4[q];
+      }
       __syncthreads();
 #pragma unroll
       for (int i = 0; i < TN; ++i)

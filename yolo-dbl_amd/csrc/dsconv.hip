@@ -69,6 +69,9 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - p.PAD, ix0 = ox0 * S - p.PAD;
   const int co0 = cs * NTN * 16;
+  __shared__ __align__(16) float s_bias[NTN * 16];
+  BiasStage<NTN * 16> bst;
+  bst.fetch(p.bias, co0, p.Cout);
 
   constexpr int TAPV = K * K * NQ;  // fp32 tap quads per chunk (392 for k7 f16: > one per thread)
   constexpr int TIT = (TAPV + 255) / 256;
@@ -123,6 +126,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
   const int nchunks = p.Cin / CC;
   load_chunk(0);
   store_chunk(0);
+  bst.commit(s_bias);
   __syncthreads();
   for (int ch = 0; ch < nchunks; ++ch) {
     const int buf = DBUF ? (ch & 1) : 0;
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void dsconv_kernel(ConvArgs<T> p, const flo
   int co[NTN];
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
-  conv_epilogue<T, NTN, TMW>(p, acc, pp, pv, co);
+  conv_epilogue<T, NTN, TMW>(p, acc, pp, pv, co, s_bias, co0);
   if constexpr (NTN == 4) {  // the tail is only launched with Cout 64 = NTN * 16 (host-checked)
     if (p.t3w) conv_tail_1x1<T, NTN, TMW>(p, acc, pp, pv, co, g);
   }
