@@ -1,8 +1,11 @@
 """Timing of ydbl_batch_max (predict()'s LoadTensor maximum) on the bench batch, 32x3x640x640 fp32, by variant
-against torch.amax.
+against torch.amax.  Warm = the batch still in the 256 MiB Infinity Cache (back-to-back calls); cold = a 512 MB
+write between calls evicts it, as the network's activations do between two predict() calls.  --variants also
+times the read orders of scripts/bmax_variants.hip (built with hipcc into abtmp/).
 
-    python scripts/bmax_bench.py
+    python scripts/bmax_bench.py [--variants]
 """
+import ctypes
 import sys
 from pathlib import Path
 
@@ -30,6 +33,21 @@ def timed(fn, reps=50):
     return best
 
 
+def timed_cold(fn, flush, reps=40):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    ts = []
+    for _ in range(reps):
+        flush.fill_(1.0)
+        a.record()
+        fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
 def main():
     x = torch.rand(32, 3, 640, 640, device="cuda")
     work = _lib.batch_max_work("cuda")
@@ -39,6 +57,35 @@ def main():
     us = timed(f)
     print(f"ydbl_batch_max: {us:7.2f} us  ({x.numel() * 4 / us / 1e6:.2f} TB/s)", flush=True)
     print(f"torch.amax: {timed(lambda: torch.amax(x)):7.2f} us", flush=True)
+    flush = torch.empty(128 * 1024 * 1024, device="cuda")
+    tb = lambda us: x.numel() * 4 / us / 1e6
+    us = timed_cold(f, flush)
+    print(f"cold ydbl_batch_max: {us:7.2f} us  ({tb(us):.2f} TB/s)", flush=True)
+    us = timed_cold(lambda: torch.amax(x), flush)
+    print(f"cold torch.amax: {us:7.2f} us  ({tb(us):.2f} TB/s)", flush=True)
+    if "--variants" not in sys.argv:
+        return
+    so = ctypes.CDLL(str(ROOT / "abtmp" / "libbmax_variants.so"))
+    so.bmax_variant.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    part = torch.empty(1 << 20, device="cuda")
+    ref = torch.amax(x).item()
+    names = {0: "contiguous", 1: "staggered", 2: "interleaved", 3: "contiguous-nt", 4: "nt+atomics"}
+    vwork = torch.zeros(66 * 64, dtype=torch.int32, device="cuda")
+    vwork.view(-1, 64)[0::2] = -2 ** 31
+    # (mode, rounds, blocks, skew | groups)
+    cases = [(0, 16, 1200, 0), (0, 8, 4800, 0), (2, 8, 4096, 0), (3, 16, 1200, 0), (3, 8, 2400, 0), (3, 32, 600, 0),
+             (3, 16, 600, 0), (3, 8, 1200, 0), (3, 16, 2400, 0), (3, 8, 4800, 0), (3, 32, 1200, 0),
+             (4, 16, 1200, 8), (4, 16, 1200, 32), (4, 16, 600, 8), (4, 32, 600, 16), (4, 8, 2400, 32)]
+    for mode, rounds, blocks, skew in cases:
+        g = lambda: so.bmax_variant(mode, rounds, x.data_ptr(), x.numel(), blocks, skew, part.data_ptr(),
+                                    vwork.data_ptr(), st)
+        us = timed_cold(g, flush)
+        part.fill_(-1.0)
+        g()
+        ok = (part[0] if mode == 4 else torch.amax(part)).item() == ref
+        print(f"cold {names[mode]:13s} R={rounds:2d} blocks={blocks:5d} skew={skew:4d}: {us:7.2f} us "
+              f"({tb(us):.2f} TB/s) {'ok' if ok else 'WRONG'}", flush=True)
 
 
 if __name__ == "__main__":

@@ -17,10 +17,15 @@ for r in 1 2; do
     done
   done
 done
-for r in 1 2; do
-  for v in base new; do
-    L=""; [ $v = base ] && L="YDBL_LIB=abtmp/libydbl_base.so"
-    env $L timeout -k 10 200 python bench.py --no-cpu-baseline --no-roofline > $T/bench_${v}_r$r.json 2>/dev/null || exit 1
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'])" $T/bench_${v}_r$r.json "bench $v r$r"
+# VIA_PREDICT=1: also bench.py --via-predict (the public predict() on the resident batch)
+MODES="session"; [ -n "$VIA_PREDICT" ] && MODES="session predict"
+for m in $MODES; do
+  A=""; [ $m = predict ] && A="--via-predict"
+  for r in 1 2; do
+    for v in base new; do
+      L=""; [ $v = base ] && L="YDBL_LIB=abtmp/libydbl_base.so"
+      env $L timeout -k 10 200 python bench.py --no-cpu-baseline --no-roofline $A > $T/bench_${m}_${v}_r$r.json 2>/dev/null || exit 1
+      python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'])" $T/bench_${m}_${v}_r$r.json "bench $m $v r$r"
+    done
   done
 done

@@ -2,8 +2,10 @@
 // for predict() on an HBM-resident batch: the batch maximum feeds the plans' input binding (include/ydbl.h
 // ydbl_input_bind), so the stem kernels scale the batch themselves and no staging copy or host sync is needed.
 //
-// One launch, HBM-bound (4 bytes per element, read once; the stems read the batch right after, so plain loads
-// that leave it in MALL).  Each workgroup reads a contiguous chunk in rounds of 16 16-byte loads per thread, the
+// One launch, HBM-bound (4 bytes per element, read once) with nontemporal loads: the batch is not in the 256 MiB
+// Infinity Cache when predict() runs (the previous call's activations evicted it) and a plain load's allocation
+// there evicts dirty activation lines first -- 63 vs 31 us cold, scripts/bmax_bench.py, profiles/r05/r05_nt_input.txt
+// (warm, back-to-back, both 26 us).  Each workgroup reads a contiguous chunk in rounds of 16 16-byte loads per thread, the
 // index clamped to the chunk's last vector instead of a masked tail (max is idempotent: a repeated element changes
 // nothing), so a thread waits on two round trips.  Workgroup maxima meet in device-scope atomicMax on an
 // order-preserving integer key (NaN mapped to the largest key: NaN propagates as in torch.max), in two levels:
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(BMAX_THREADS) void batch_max_kernel(const float* __
     for (int64_t base = lo + threadIdx.x; base <= hi; base += BMAX_ROUND * BMAX_THREADS) {
       f32x4 v[BMAX_ROUND];
 #pragma unroll
-      for (int u = 0; u < BMAX_ROUND; ++u) v[u] = xv[min(base + u * BMAX_THREADS, hi)];
+      for (int u = 0; u < BMAX_ROUND; ++u) v[u] = __builtin_nontemporal_load(xv + min(base + u * BMAX_THREADS, hi));
 #pragma unroll
       for (int u = 0; u < BMAX_ROUND; ++u)
 #pragma unroll

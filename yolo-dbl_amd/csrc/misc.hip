@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void input_kernel(const float* __restrict__ x,
 #pragma unroll
     for (int q = 0; q < Vec<T>::N; ++q) {
       const int ch = c0 + q;
-      v[q] = ch < c ? x[(b * c + ch) * hw + off] * scale : 0.f;
+      v[q] = ch < c ? __builtin_nontemporal_load(x + (b * c + ch) * hw + off) * scale : 0.f;
     }
     store_f<Vec<T>::N>(yp + c0, v);
   }

@@ -58,8 +58,9 @@ __global__ __launch_bounds__(256) void stem_kernel(const float* __restrict__ x, 
         const int iy = iy0 + r;
         const int iyc = min(max(iy, 0), H - 1);
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-          v[u][c] = *reinterpret_cast<const f32x4*>(xb + c * plane + (int64_t)iyc * W + 4 * gx);
+        for (int c = 0; c < 3; ++c)  // the batch, read once: nontemporal (batchmax.hip)
+          v[u][c] = __builtin_nontemporal_load(
+              reinterpret_cast<const f32x4*>(xb + c * plane + (int64_t)iyc * W + 4 * gx));
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {

@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   constexpr int IT = (TASKS + 255) / 256;
   f32x4 v[IT][3];
   bool okv[IT];  // the task's pixels lie inside the image (record slot 3 = 1: the folded bias)
-  auto load_window = [&](const Tile& tl) {
+  auto load_window = [&](const Tile& tl) {  // the batch, read once: nontemporal loads (batchmax.hip)
     const float* xb = x + (int64_t)tl.img * 3 * plane;
     if constexpr (V4) {
       const int A = tl.X0 - 3;
@@ -158,7 +158,8 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
         const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          v[u][c] = ok ? *reinterpret_cast<const f32x4*>(xb + c * plane + o) : f32x4{0.f, 0.f, 0.f, 0.f};
+          v[u][c] = ok ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xb + c * plane + o))
+                       : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     } else {
 #pragma unroll
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
         okv[u] = ok;
         const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) v[u][ch][0] = ok ? xb[ch * plane + o] : 0.f;
+        for (int ch = 0; ch < 3; ++ch) v[u][ch][0] = ok ? __builtin_nontemporal_load(xb + ch * plane + o) : 0.f;
       }
     }
   };
