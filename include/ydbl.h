@@ -373,7 +373,8 @@ int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream);
  * intermediate never leaves LDS.  x, y: NHWC fp16 views of the same shape with x.c == y.c == c
  * (c = 16, 32 or 64), y must not alias x.  params: device blob of ydbl_bottleneck_params_size(c)
  * bytes filled on the HOST by ydbl_bottleneck_pack from fp32 w1 [c/2][c][3][3], b1 [c/2],
- * w2 [c][c/2][3][3], b2 [c] (BN folded).  tile_h: 0 = auto, else 8 or 16 output rows per workgroup. */
+ * w2 [c][c/2][3][3], b2 [c] (BN folded).  tile_h: 0 = auto, else 8 or 16 output rows per workgroup (or 9 for
+ * c 64 / c_mid 32). */
 typedef struct {
   ydbl_view x, y;
   int32_t c;

@@ -174,7 +174,8 @@ CASES = [case_dsc3k(16, 128, 20), case_hg(16, 64, 40), case_hg(16, 128, 40), cas
          case_conv(16, 128, 64, 1, 1, 80, 80), case_conv(16, 64, 128, 1, 1, 80, 80),
          case_conv(16, 384, 128, 1, 1, 40, 40), case_conv(16, 320, 128, 1, 1, 40, 40), case_conv(16, 128, 192, 1, 1, 40, 40),
          case_conv(16, 128, 128, 1, 1, 40, 40), case_conv(16, 384, 256, 1, 1, 20, 20), case_conv(16, 128, 256, 1, 1, 20, 20),
-         case_conv(16, 64, 64, 3, 1, 20, 20), case_bneck(16, 16, 320), case_bneck(16, 32, 160), case_bneck(16, 64, 80)]
+         case_conv(16, 64, 64, 3, 1, 20, 20), case_bneck(16, 16, 320), case_bneck(16, 32, 160), case_bneck(16, 64, 80),
+         case_bneck(32, 64, 80)]
 
 
 def main():

@@ -562,7 +562,10 @@ def test_stem2(c0, n, h, w):
     (64, 2, 80, 80, False, 0, 0, 64), (64, 3, 37, 29, False, 8, 8, 64), (64, 1, 5, 3, True, 0, 0, 64),
     # more tiles than resident workgroups (ragged maps, channel slices): several tiles per workgroup wherever the
     # walk is persistent
-    (16, 4, 320, 320, True, 16, 8, 0), (32, 3, 165, 158, True, 0, 0, 0), (16, 2, 331, 318, False, 0, 8, 0)])
+    (16, 4, 320, 320, True, 16, 8, 0), (32, 3, 165, 158, True, 0, 0, 0), (16, 2, 331, 318, False, 0, 8, 0),
+    # 9-row tiles (c 64 / c_mid 32): forced, ragged, and the auto choice at DBL-n's 80^2 bs16 sub-batch
+    (64, 2, 80, 80, True, 9, 0, 0), (64, 3, 37, 29, True, 9, 8, 0), (64, 1, 10, 17, False, 9, 0, 0),
+    (64, 16, 80, 80, True, 0, 0, 0)])
 def test_bottleneck_fused(c, n, h, w, add, tile_h, cs_extra, cm):
     """ydbl_bottleneck_nhwc (cv1 3x3 c->c_mid, cv2 3x3 c_mid->c, SiLU, optional x + ..., fp16) vs the two
     convs in fp32 on fp16-rounded operands, the intermediate rounded to fp16 as the unfused path stores it
@@ -642,7 +645,7 @@ def test_bottleneck_rejects_bad_shapes():
     plan = _plan(torch.float16)
     params = torch.zeros(64, dtype=torch.uint8, device=DEV)
     for c, xs, ys, tile_h in [(48, (1, 8, 8, 48), (1, 8, 8, 48), 0), (32, (1, 8, 8, 32), (1, 8, 9, 32), 0),
-                              (32, (1, 8, 8, 32), (1, 8, 8, 32), 4)]:
+                              (32, (1, 8, 8, 32), (1, 8, 8, 32), 4), (32, (1, 8, 8, 32), (1, 8, 8, 32), 9)]:
         xv, yv = plan.alloc(*xs), plan.alloc(*ys)
         d = _lib.BottleneckDesc(xv.struct(), yv.struct(), c, 1, tile_h, params.data_ptr())
         assert _lib.lib.ydbl_bottleneck_nhwc(ctypes.byref(d), None) != 0

@@ -488,12 +488,38 @@ static int bneck_go(const ydbl_bottleneck_desc* d, hipStream_t s) {
   return check_launch("ydbl_bottleneck_nhwc");
 }
 
+// workgroups of a bneck_kernel instantiation resident per CU x the CUs (queried once per instantiation)
+template <int C, int CMID, int TH>
+static int64_t bneck_slots() {
+  static int64_t slots = [] {
+    int dev = 0, cus = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, bneck_kernel<C, CMID, TH, true>, 256, 0) != hipSuccess)
+      return (int64_t)0;
+    return (int64_t)cus * per;
+  }();
+  return slots;
+}
+
 template <int C, int CMID>
 static int bneck_dispatch(const ydbl_bottleneck_desc* d, hipStream_t s) {
   // 16-row tiles halve the halo recompute; 8-row tiles when 16-row ones leave the chip under-filled
   // (and always for c_mid = 64: its 16-row tile would need 102 KB of LDS, one workgroup per CU)
   const int64_t t16 = cdiv(d->y.h, 16) * cdiv(d->y.w, 16) * (int64_t)d->y.n;
-  const int th = d->tile_h ? d->tile_h : (t16 >= 1024 && CMID < 64 ? 16 : 8);
+  int th = d->tile_h ? d->tile_h : (t16 >= 1024 && CMID < 64 ? 16 : 8);
+  if constexpr (C == 64 && CMID == 32) {
+    // 9-row tiles (51 KB of LDS: still 3 workgroups per CU) when they take fewer rounds of the resident
+    // workgroups: DBL-n's 80^2 Bottlenecks at bs16 are 800 8-row tiles on 768 slots -- a second round of 32 --
+    // and 720 9-row ones in one (a round priced by its cv1 rows, TH + 2)
+    if (!d->tile_h && th == 8) {
+      const int64_t s8 = bneck_slots<C, CMID, 8>(), s9 = bneck_slots<C, CMID, 9>();
+      const int64_t t8 = cdiv(d->y.h, 8) * cdiv(d->y.w, 16) * (int64_t)d->y.n;
+      const int64_t t9 = cdiv(d->y.h, 9) * cdiv(d->y.w, 16) * (int64_t)d->y.n;
+      if (s8 > 0 && s9 > 0 && cdiv(t9, s9) * 11 < cdiv(t8, s8) * 10) th = 9;
+    }
+    if (th == 9) return bneck_go<C, CMID, 9>(d, s);
+  }
   return th == 16 ? bneck_go<C, CMID, 16>(d, s) : bneck_go<C, CMID, 8>(d, s);
 }
 
@@ -509,7 +535,8 @@ extern "C" int ydbl_bottleneck_nhwc(const ydbl_bottleneck_desc* d, void* stream)
   if (d->x.n != d->y.n || d->x.h != d->y.h || d->x.w != d->y.w)
     return fail(YDBL_EINVAL, "bottleneck: x and y shapes differ");
   if (d->y.n < 1 || d->y.h < 1 || d->y.w < 1) return fail(YDBL_EINVAL, "bottleneck: empty input");
-  if (d->tile_h != 0 && d->tile_h != 8 && d->tile_h != 16) return fail(YDBL_EINVAL, "bottleneck: tile_h must be 0, 8 or 16");
+  if (d->tile_h != 0 && d->tile_h != 8 && d->tile_h != 16 && !(d->tile_h == 9 && c == 64 && cm == 32))
+    return fail(YDBL_EINVAL, "bottleneck: tile_h must be 0, 8 or 16 (or 9 for (c, c_mid) = (64, 32))");
   if (d->x.ptr == d->y.ptr) return fail(YDBL_EINVAL, "bottleneck: in-place is not supported (halo reads)");
   hipStream_t s = as_stream(stream);
   if (c == 16 && cm == 8) return bneck_dispatch<16, 8>(d, s);
