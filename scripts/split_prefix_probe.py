@@ -4,7 +4,8 @@ first K launches and a graph of the two bs16 sub-batch plans' first K launches a
 both (replays alternating, several rounds).  A prefix that is cheaper at bs32 could run as one pass before the
 graph forks into the two sub-batch branches.
 
-    python scripts/split_prefix_probe.py [K ...]
+    python scripts/split_prefix_probe.py [K ...]            (bs32 pass vs 2 branches)
+    python scripts/split_prefix_probe.py --s4 [K ...]       (2 bs16 branches vs 4 bs8 branches)
 """
 import sys
 import time
@@ -23,7 +24,8 @@ from ydbl.utils.synthetic import blob_images, load_trained  # noqa: E402
 
 
 def main():
-    ks = [int(a) for a in sys.argv[1:]] or [1, 2, 5, 9, 10, 12, 28]
+    s4 = "--s4" in sys.argv
+    ks = [int(a) for a in sys.argv[1:] if a != "--s4"] or [1, 2, 5, 9, 10, 12, 28]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
@@ -31,7 +33,7 @@ def main():
     load_trained(model.model, ROOT / "tests" / "golden" / "trained_yolov13n_DBL_nc3.npz")
     kw = dict(half=True, conf=0.25, iou=0.7, max_det=300, device=dev)
     s2 = model.session(32, 640, 640, streams=2, **kw)
-    s1 = model.session(32, 640, 640, streams=1, **kw)
+    s1 = model.session(32, 640, 640, streams=4 if s4 else 1, **kw)
     x = blob_images(32, 640, seed=1234).to(dev)
     s2.load(x)
     s1.load(x)
@@ -40,6 +42,7 @@ def main():
         s1.launch()
     torch.cuda.synchronize(dev)
     p1, p2 = s1.plan, s2.plans
+    p4 = s1.plans if s4 else None
     print("launches:", ", ".join(f"{i}:{st.what}" for i, st in enumerate(p1.steps[:30])), flush=True)
 
     def single(k):
@@ -48,16 +51,20 @@ def main():
             run_steps(p1, p1.steps[:k], torch.cuda.current_stream(dev).cuda_stream)
         return g
 
-    def branches(k):
-        side = torch.cuda.Stream(dev)
+    def branches(k, plans=None):
+        plans = plans or p2
+        sides = [torch.cuda.Stream(dev) for _ in plans[1:]]
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             cap = torch.cuda.current_stream(dev)
-            side.wait_stream(cap)
-            run_steps(p2[0], p2[0].steps[:k], cap.cuda_stream)
-            with torch.cuda.stream(side):
-                run_steps(p2[1], p2[1].steps[:k], side.cuda_stream)
-            cap.wait_stream(side)
+            for side in sides:
+                side.wait_stream(cap)
+            run_steps(plans[0], plans[0].steps[:k], cap.cuda_stream)
+            for pl, side in zip(plans[1:], sides):
+                with torch.cuda.stream(side):
+                    run_steps(pl, pl.steps[:k], side.cuda_stream)
+            for side in sides:
+                cap.wait_stream(side)
         return g
 
     def t(g, n=40):
@@ -70,15 +77,16 @@ def main():
         torch.cuda.synchronize(dev)
         return (time.perf_counter() - t0) / n * 1e6
 
-    for k in ks:
-        gs, gb = single(k), branches(k)
+    for k in [min(k, len(p1.steps)) for k in ks]:
+        gs, gb = (branches(k, p4) if s4 else single(k)), branches(k)
         a, b = [], []
         for _ in range(4):
             a.append(t(gs))
             b.append(t(gb))
         a.sort()
         b.sort()
-        print(f"first {k:2d} launches (to {p1.steps[k - 1].what}): bs32 one pass {a[1]:8.1f} us, "
+        print(f"first {k:2d} launches (to {p1.steps[k - 1].what}): {'4 bs8 branches' if s4 else 'bs32 one pass'} "
+              f"{a[1]:8.1f} us, "
               f"two bs16 branches {b[1]:8.1f} us  ({100 * (a[1] / b[1] - 1):+.1f} %)", flush=True)
 
 
