@@ -333,7 +333,11 @@ int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream);
  * Semantics of U/utils/ops.py:278-310 + torchvision nms: candidates above max_nms are cut to the
  * max_nms highest scores; boxes offset by cls*max_wh (0 if agnostic); stable descending sort;
  * suppress j if IoU(i,j) > iou_thres (double compare); keep <= max_det.
- * clip_w/clip_h > 0: clamp kept boxes to [0,w]x[0,h] (scale_boxes with gain 1, pad 0). */
+ * clip_w/clip_h > 0: clamp kept boxes to [0,w]x[0,h] (scale_boxes with gain 1, pad 0).
+ * per_image (schedule only, same output): 0 = the class-split sweep for non-agnostic NMS (one workgroup per image
+ * and class group + a merge: the faster form when images carry thousands of candidates, e.g. validation's
+ * conf 0.001); nonzero = one workgroup per image (the faster form when every image has at most 1024 candidates,
+ * the pair-matrix path: predict's conf 0.25 -- DBL-n bs32 +0.8 %, profiles/r05/r05_nms_per_image_ab.txt). */
 typedef struct {
   const float* cand_box; const float* cand_score; const int32_t* cand_cls; const int32_t* cand_idx;
   const int32_t* cand_count;
@@ -345,6 +349,7 @@ typedef struct {
   float* out; int32_t* out_count;
   void* workspace;
   int64_t out_stride, count_stride;
+  int32_t per_image;
 } ydbl_nms_desc;
 int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms);
 int ydbl_nms(const ydbl_nms_desc* d, void* stream);

@@ -392,18 +392,19 @@ def test_nms_paths_agree_on_model_candidates(golden_dir, monkeypatch, groups):
     cap = sess.cand_score.shape[1]
     ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device="cuda")
     outs = []
-    for fast in ("1", "0"):
+    for fast, per_image in (("1", 0), ("0", 0), ("1", 1)):  # per_image 1: the session's own schedule at conf .25
         monkeypatch.setenv("YDBL_NMS_FAST", fast)
         monkeypatch.setenv("YDBL_NMS_GROUPS", groups)
         out = torch.full((B, 300, 6), -1.0, device="cuda")
         cnt = torch.full((B,), -1, dtype=torch.int32, device="cuda")
         nd = NmsDesc(sess.cand_box.data_ptr(), sess.cand_score.data_ptr(), sess.cand_cls.data_ptr(),
                      sess.cand_idx.data_ptr(), sess.cand_count.data_ptr(), B, cap, 0.7, 300, 30000, 0, 7680.0,
-                     640.0, 640.0, out.data_ptr(), cnt.data_ptr(), ws.data_ptr())
+                     640.0, 640.0, out.data_ptr(), cnt.data_ptr(), ws.data_ptr(), per_image=per_image)
         _lib.check(_lib.lib.ydbl_nms(nd, torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
         outs.append((out, cnt))
-    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][0], outs[1][0])
+    for o in outs[1:]:
+        assert torch.equal(outs[0][1], o[1]) and torch.equal(outs[0][0], o[0])
     assert torch.equal(outs[0][1], sess.count) and torch.equal(outs[0][0], sess.det)
 
 

@@ -1079,7 +1079,7 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   if (a.fast) nms_pair_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
   // class-split sweep + merge (non-agnostic); the one-workgroup-per-image form for agnostic NMS or on request
   const char* ev = getenv("YDBL_NMS_GROUPS");  // A/B switch (read per launch: tests): 0 = one workgroup per image
-  if (d->agnostic || (ev && *ev == '0')) {
+  if (d->agnostic || d->per_image || (ev && *ev == '0')) {
     nms_kernel<false><<<d->n, NMS_THREADS, 0, s>>>(a);
   } else {
     nms_kernel<true><<<(unsigned)((int64_t)d->n * NMS_GROUPS), NMS_THREADS, 0, s>>>(a);

@@ -78,7 +78,7 @@ class NmsDesc(C.Structure):
                 ("iou_thres", C.c_double), ("max_det", C.c_int32), ("max_nms", C.c_int32), ("agnostic", C.c_int32),
                 ("max_wh", C.c_float), ("clip_w", C.c_float), ("clip_h", C.c_float), ("out", C.c_void_p),
                 ("out_count", C.c_void_p), ("workspace", C.c_void_p), ("out_stride", C.c_int64),
-                ("count_stride", C.c_int64)]
+                ("count_stride", C.c_int64), ("per_image", C.c_int32)]
 
 
 class InputBind(C.Structure):

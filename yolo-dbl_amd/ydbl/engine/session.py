@@ -29,6 +29,13 @@ def default_streams(batch: int) -> int:
     return 2 if batch >= SPLIT_MIN_BATCH else 1
 
 
+# Score threshold from which the NMS runs one workgroup per image instead of the class-split sweep (ydbl_nms_desc
+# per_image): at predict-like thresholds every image has at most 1024 candidates (the pair-matrix path; DBL-n bs32
+# at conf 0.25: 645 at most) and the split's extra workgroups and merge cost +0.8 % of the step
+# (profiles/r05/r05_nms_per_image_ab.txt); validation's conf 0.001 keeps the split.
+PER_IMAGE_NMS_CONF = 0.1
+
+
 class BoundOutputs:
     """A predict() call's outputs in a session's binding slot (DetectSession.launch_bound): det [B, max_det, 6],
     count [B] and LoadTensor's scale, valid as views of the slot until detach() copies them out (on first access, or
@@ -158,7 +165,7 @@ class DetectSession:
                      self.cand_idx.data_ptr(), self.cand_count.data_ptr(), batch, cap, self.iou, self.max_det,
                      int(max_nms), int(bool(agnostic)), float(max_wh), float(w) if clip else 0.0,
                      float(h) if clip else 0.0, self.det.data_ptr(), self.count.data_ptr(), ws.data_ptr(),
-                     self.det.stride(0), self.count.stride(0))
+                     self.det.stride(0), self.count.stride(0), int(self.conf >= PER_IMAGE_NMS_CONF))
         if nms:  # nms=False: forward + decode only (DetectionModel.forward -> (y, feats))
             plan.launch("ydbl_nms", nd, what="NMS", keep=[nd])
         self.plan = plan
