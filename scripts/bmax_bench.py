@@ -70,20 +70,33 @@ def main():
                                 ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     part = torch.empty(1 << 20, device="cuda")
     ref = torch.amax(x).item()
-    names = {0: "contiguous", 1: "staggered", 2: "interleaved", 3: "contiguous-nt", 4: "nt+atomics"}
-    vwork = torch.zeros(66 * 64, dtype=torch.int32, device="cuda")
+    names = {0: "contiguous", 1: "staggered", 2: "interleaved", 3: "contiguous-nt", 4: "nt+atomics", 5: "nt+keys"}
+    vwork = torch.zeros(260 * 64, dtype=torch.int32, device="cuda")
     vwork.view(-1, 64)[0::2] = -2 ** 31
     # (mode, rounds, blocks, skew | groups)
     cases = [(0, 16, 1200, 0), (0, 8, 4800, 0), (2, 8, 4096, 0), (3, 16, 1200, 0), (3, 8, 2400, 0), (3, 32, 600, 0),
              (3, 16, 600, 0), (3, 8, 1200, 0), (3, 16, 2400, 0), (3, 8, 4800, 0), (3, 32, 1200, 0),
              (4, 16, 1200, 8), (4, 16, 1200, 32), (4, 16, 600, 8), (4, 32, 600, 16), (4, 8, 2400, 32)]
+    if "--atomics" in sys.argv:  # the merge's group count at the larger grids
+        cases = [(3, 8, 4800, 0), (3, 8, 9600, 0), (3, 4, 9600, 0), (4, 8, 4800, 8), (4, 8, 4800, 32),
+                 (4, 8, 4800, 64), (4, 8, 2400, 32), (4, 16, 2400, 32), (4, 16, 1200, 32), (4, 8, 9600, 64),
+                 (5, 16, 1200, 8), (5, 16, 1200, 32), (5, 8, 4800, 32), (5, 4, 9600, 64), (5, 4, 9600, 8)]
     for mode, rounds, blocks, skew in cases:
         g = lambda: so.bmax_variant(mode, rounds, x.data_ptr(), x.numel(), blocks, skew, part.data_ptr(),
                                     vwork.data_ptr(), st)
         us = timed_cold(g, flush)
         part.fill_(-1.0)
         g()
-        ok = (part[0] if mode == 4 else torch.amax(part)).item() == ref
+        if mode == 5:  # the keys hold order keys of non-negative maxima: the float bits themselves
+            keys = vwork[:skew * 64:64].clone()
+            vwork[:skew * 64:64] = -2 ** 31
+            g()
+            got = vwork[:skew * 64:64].view(torch.float32).max()
+            vwork.view(-1, 64)[0::2] = -2 ** 31
+            vwork.view(-1, 64)[1::2] = 0
+            ok = got.item() == ref
+        else:
+            ok = (part[0] if mode == 4 else torch.amax(part)).item() == ref
         print(f"cold {names[mode]:13s} R={rounds:2d} blocks={blocks:5d} skew={skew:4d}: {us:7.2f} us "
               f"({tb(us):.2f} TB/s) {'ok' if ok else 'WRONG'}", flush=True)
 

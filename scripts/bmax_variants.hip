@@ -84,6 +84,10 @@ __global__ __launch_bounds__(NT) void bmax_var(const f32x4* __restrict__ xv, int
     const int r = atomicExch(key, (int)0x80000000);
     atomicExch(tick, 0);
     part[0] = __int_as_float(r >= 0 ? r : r ^ 0x7fffffff);
+  } else if constexpr (MODE == 5) {
+    // non-returning atomicMax into `groups` keys (64 ints apart), keys of the other parity (work + 8192) reset
+    if (threadIdx.x == 0) atomicMax(work + (blockIdx.x % groups) * 64, order_key(m));
+    if (blockIdx.x == 0 && threadIdx.x < groups) work[8192 + threadIdx.x * 64] = (int)0x80000000;
   } else {
     if (threadIdx.x == 0) part[blockIdx.x] = m;
   }
@@ -94,7 +98,7 @@ static void launch(const float* x, int64_t n, int blocks, int64_t skew, float* p
   const int64_t nv = n / 4;
   int64_t chunk = (nv + blocks - 1) / blocks;
   if (MODE == 1) chunk += skew;
-  const int groups = MODE == 4 ? (int)skew : 1;
+  const int groups = MODE >= 4 ? (int)skew : 1;
   const int64_t need = (nv + chunk - 1) / chunk;
   const int grid = MODE == 1 ? (int)need : blocks;
   bmax_var<MODE, R><<<grid, NT, 0, s>>>(reinterpret_cast<const f32x4*>(x), nv, chunk, part, work, groups);
@@ -107,12 +111,14 @@ extern "C" int bmax_variant(int mode, int rounds, const float* x, int64_t n, int
   if (mode == M) {                                                      \
     if (rounds == 32) launch<M, 32>(x, n, blocks, skew, part, work, s); \
     else if (rounds == 16) launch<M, 16>(x, n, blocks, skew, part, work, s); \
-    else launch<M, 8>(x, n, blocks, skew, part, work, s);               \
+    else if (rounds == 8) launch<M, 8>(x, n, blocks, skew, part, work, s); \
+    else launch<M, 4>(x, n, blocks, skew, part, work, s);               \
   }
   BMAX_CASE(0)
   BMAX_CASE(1)
   BMAX_CASE(2)
   BMAX_CASE(3)
   BMAX_CASE(4)
+  BMAX_CASE(5)
   return (int)hipGetLastError();
 }
