@@ -195,6 +195,22 @@ def test_predict_reads_device_tensor_in_place(golden_dir, batch, streams):
         assert torch.equal(r.boxes.data, got01[i])
 
 
+def test_predict_fp16_device_batch_0_255(golden_dir):
+    """A half-precision device batch in [0, 255] takes the staging copy with LoadTensor's rule computed in fp32,
+    im.float() / 255.0 (U/data/loaders.py:561-566) -- not x * (1/255) rounded to fp16 first: detections
+    bit-equal to the same batch passed as fp32; Results.orig_img is the fp32-scaled image."""
+    from ydbl.utils.synthetic import blob_images
+
+    p, _ = _models("yolov13n_DBL.yaml", 3, golden_dir)
+    x16 = (blob_images(4, 160, seed=78) * 255.0).round().half().cuda()
+    want = [r.boxes.data.clone() for r in p.predict(x16.float(), half=True, conf=0.05)]
+    res = p.predict(x16, half=True, conf=0.05)
+    assert sum(len(w) for w in want) > 0
+    for r, w in zip(res, want):
+        assert torch.equal(r.boxes.data, w)
+    assert torch.equal(res[1].orig_img.cpu(), (x16[1].float() / 255.0).permute(1, 2, 0).cpu())
+
+
 def test_predict_back_to_back_calls_keep_their_batches(golden_dir):
     """Back-to-back predict() calls on different device batches without a sync in between (the in-place path
     alternates two binding slots on the session's own stream while the caller's stream runs ahead): every call's

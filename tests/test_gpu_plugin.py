@@ -135,3 +135,47 @@ def test_forward_only_plugin_end_to_end(golden_dir, monkeypatch, streams):
     ph(x.cuda())
     torch.cuda.synchronize()
     assert (ph.pred.cpu() - s.pred.cpu()).abs()[:, :4].max().item() <= 2 * tb
+
+
+def _plugin_model(golden_dir, monkeypatch):
+    import oracle.model as om
+    from ydbl import YOLO
+    from ydbl.nn import tasks
+    from ydbl.utils.synthetic import load_trained
+
+    monkeypatch.setitem(tasks.REGISTRY, "LSKblock", om.LSKblock)
+    torch.manual_seed(0)
+    q = YOLO("yolov13n_DBL.yaml", nc=3)
+    load_trained(q.model, golden_dir / "trained_yolov13n_DBL_nc3.npz")
+    return q
+
+
+def test_forward_only_plugin_eager_default_stream(golden_dir, monkeypatch):
+    """use_graph=False runs the plan eagerly on torch's current stream -- the default (null) stream here, whose
+    handle is 0: the plugin step must run on it, bit-equal to the captured run of the same session
+    layout."""
+    from ydbl.utils.synthetic import blob_images
+
+    q = _plugin_model(golden_dir, monkeypatch)
+    x = blob_images(2, 160, seed=3).cuda()
+    assert torch.cuda.current_stream().cuda_stream == torch.cuda.default_stream().cuda_stream
+    se = q.session(2, 160, 160, half=False, conf=0.05, keep_pred=True, use_graph=False)
+    se(x)
+    sg = q.session(2, 160, 160, half=False, conf=0.05, keep_pred=True, use_graph=True)
+    sg(x)
+    torch.cuda.synchronize()
+    assert torch.equal(se.pred, sg.pred)
+
+
+def test_forward_only_plugin_fp8_calibration(golden_dir, monkeypatch):
+    """fp8 calibration runs the plan step by step on the current stream (Plan.run_observed): a plan holding a
+    forward-only plugin must calibrate and then replay."""
+    from ydbl.utils.synthetic import blob_images
+
+    q = _plugin_model(golden_dir, monkeypatch)
+    x = blob_images(2, 160, seed=3).cuda()
+    s = q.session(2, 160, 160, half=True, fp8=True, conf=0.05, keep_pred=True, use_graph=True)
+    s(x)
+    torch.cuda.synchronize()
+    assert s.fp8_ready and s.fp8_mac_fraction > 0
+    assert torch.isfinite(s.pred).all()

@@ -78,6 +78,24 @@ def check_tensor_source(im, stride: int = 32) -> torch.Tensor:
 _SCALES = {}
 
 
+def _calib_key(cal):
+    """Session-cache key of an fp8 calibration: its path, or a fingerprint of its content (not id(): a new object
+    for the same record would compile a new session, and a recycled id could hit a session of another record)."""
+    if cal is None or isinstance(cal, (str, Path)):
+        return None if cal is None else str(cal)
+    fp = getattr(cal, "_ydbl_fingerprint", None)
+    if fp is None:
+        import hashlib
+        import json
+
+        fp = hashlib.sha1(json.dumps(cal.to_json(), sort_keys=True).encode()).hexdigest()
+        try:
+            cal._ydbl_fingerprint = fp
+        except AttributeError:
+            pass
+    return fp
+
+
 def _scale_consts(dev):
     """(1.0, fp32(1/255)) as 0-dim fp32 tensors on `dev` (made once)."""
     c = _SCALES.get(dev)
@@ -96,7 +114,7 @@ class _LazyHWC:
     def __getitem__(self, i):
         if self.hwc is None:
             scale = self.scale() if callable(self.scale) else self.scale
-            x = self.im.float() if scale is None else self.im * scale
+            x = self.im.float() if scale is None else self.im.float() * scale
             self.hwc = x.permute(0, 2, 3, 1)
         return self.hwc[i]
 
@@ -214,7 +232,7 @@ class Model:
         key = (batch, h, w, dtype, float(conf), float(iou), int(max_det), bool(agnostic),
                tuple(classes) if classes is not None else None, bool(multi_label), str(dev), keep_pred, use_graph,
                float(fp8), bool(clip), int(streams), gather_rows, bool(nms),
-               str(fp8_calibration) if isinstance(fp8_calibration, (str, Path)) else id(fp8_calibration),
+               _calib_key(fp8_calibration),
                # the remaining YDBL_* switches (plan-builder fusions in ydbl.nn.modules; YDBL_DS_LEAN / YDBL_NMS_*
                # in the C-ABI) are read at plan build or at each launch, so a captured graph keeps the routing of
                # its capture: a different switch setting is a different session

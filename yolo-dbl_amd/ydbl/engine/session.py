@@ -41,11 +41,14 @@ class BoundOutputs:
     count [B] and LoadTensor's scale, valid as views of the slot until detach() copies them out (on first access, or
     when the slot comes round again while this object is alive)."""
 
-    def __init__(self, det, count, flat, scale):
+    def __init__(self, det, count, flat, scale, event=None):
         self.det, self.count, self.flat, self.scale, self.own = det, count, flat, scale, False
+        self.event = event  # recorded after the replay that wrote the slot
 
     def detach(self):
         if not self.own:
+            if self.event is not None:  # the copy may be issued from another stream than the replay's
+                torch.cuda.current_stream(self.flat.device).wait_event(self.event)
             flat = self.flat.clone()
             n = self.det.numel()
             self.det, self.count = flat[:n].view(self.det.shape), flat[n:].view(torch.int32)
@@ -103,7 +106,8 @@ class DetectSession:
         # own det | count outputs, kept until the slot comes round again (then copied if its Results still live)
         self._bound = None  # the last tensor launch_bound() read (introspection)
         self._calls, self._slot_ptrs, self._pgraph, self._pout, self._pheld = 0, {}, {}, {}, {}
-        self._max_work = None
+        self._max_work = {}  # per binding slot: the batch-max kernel's tickets are reset by its last block
+        self._last_ev = None  # the last launch_bound() replay: the slots share the plans' activation buffers
         if _outputs is None and gather_rows is not None:
             # one record per image [det (max_det*6 fp32) | count (int32) | pad]: the boxes and counts of a batch-
             # sharded predict leave the GPU in ONE all-gather (ydbl.parallel); rows >= batch stay empty padding
@@ -224,6 +228,8 @@ class DetectSession:
     def can_bind(self, x: torch.Tensor) -> bool:
         """launch_bound() takes x: a contiguous fp32 tensor of the session's shape on its device, every sub-batch 16-byte
         aligned (the stem kernels' vector loads)."""
+        if self.records is not None:  # gather_rows: the NMS writes record rows (out_stride = record width), not slots
+            return False
         if (not isinstance(x, torch.Tensor) or x.dtype != torch.float32 or x.device != self.det.device
                 or not x.is_contiguous() or tuple(x.shape) != (self.batch, 3, self.h, self.w)
                 or (self.fp8 and not self.fp8_ready)):  # (an uncalibrated fp8 session calibrates on a loaded batch)
@@ -277,13 +283,13 @@ class DetectSession:
         if g is None:
             if self.fp8 and not self.fp8_ready:
                 self.calibrate_fp8(calibration=self.fp8_calibration)
-            if self._max_work is None:
-                self._max_work = _lib.batch_max_work(dev)
+            if k not in self._max_work:
+                self._max_work[k] = _lib.batch_max_work(dev)
             det, count, flat = _det_count(self.batch, self.max_det, dev)
             scale = torch.empty(1, dtype=torch.float32, device=dev)
             self._pout[k] = (det, count, flat, scale)
             pre = Plan(dev, self.dtype)
-            pre.launch("ydbl_batch_max_bound", self.bind_ptrs[k, 0:1].data_ptr(), x.numel(), self._max_work.data_ptr(),
+            pre.launch("ydbl_batch_max_bound", self.bind_ptrs[k, 0:1].data_ptr(), x.numel(), self._max_work[k].data_ptr(),
                        self.bind_amax[k].data_ptr(), scale.data_ptr(), what="LoadTensor.max")
             self._set_slot(k, det, count)
             if self.use_graph:
@@ -292,9 +298,15 @@ class DetectSession:
                 g = _EagerSlot(self, k, pre)
             self._set_slot(0)
             self._pgraph[k] = g
+        cur = torch.cuda.current_stream(dev)
+        if self._last_ev is not None:  # a replay issued from another stream must finish first (shared activations)
+            cur.wait_event(self._last_ev)
         g.replay()
+        ev = torch.cuda.Event()
+        ev.record(cur)
+        self._last_ev = ev
         det, count, flat, scale = self._pout[k]
-        out = BoundOutputs(det, count, flat, scale)
+        out = BoundOutputs(det, count, flat, scale, ev)
         self._pheld[k] = weakref.ref(out)
         self._bound = x
         return out
@@ -314,8 +326,8 @@ class DetectSession:
             raise ValueError(f"input shape {tuple(x.shape)} != session shape {tuple(self.compiled.input.shape)}")
         if scale is None:
             self.compiled.input.copy_(x, non_blocking=True)
-        else:
-            torch.mul(x, scale, out=self.compiled.input)
+        else:  # fp32 before the scale: x.float() / 255.0 as LoadTensor computes it (U/data/loaders.py:566)
+            torch.mul(x if x.dtype == torch.float32 else x.float(), scale, out=self.compiled.input)
 
     def calibrate_fp8(self, x: torch.Tensor | None = None, fraction: float | None = None, calibration=None) -> int:
         """Switch the dense convs to e4m3 operands (ydbl.quant).  calibration (an ydbl.quant.Fp8Calibration or the

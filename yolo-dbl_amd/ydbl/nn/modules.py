@@ -447,7 +447,10 @@ def emit_torch(m: nn.Module, plan: Plan, x, out: TV | None = None) -> TV:
     dm.eval()
 
     def step(stream):
-        with torch.cuda.stream(torch.cuda.ExternalStream(stream.value, device=plan.device)), torch.no_grad():
+        # handle 0 (c_void_p value None) is the null stream: eager runs on torch's default stream pass it
+        ts = (torch.cuda.ExternalStream(stream.value, device=plan.device) if stream.value
+              else torch.cuda.default_stream(plan.device))
+        with torch.cuda.stream(ts), torch.no_grad():
             ins = [v.nchw() for v in xs]
             y.nchw().copy_(dm(ins if multi else ins[0]))
         return 0
