@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round 6: per-kernel split of ydbl_nms on the wide path (rocprofv3 kernel stats per synthetic case).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; T=gpurun_out/r06_nmsprof; mkdir -p $T; export TMPDIR=/tmp
+set -o pipefail
+for c in 0 3 6; do
+  timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $T/p$c -o run -- python scripts/nms_wide_bench.py $c 1 1 \
+      > $T/p$c.log 2>&1 || exit 1
+  python scripts/rocpd_stats.py $T/p$c/run_results.db > $T/case${c}_kernel_stats.csv || exit 1
+done

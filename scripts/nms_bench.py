@@ -39,7 +39,7 @@ def run(counts, nc=3, A=8400, reps=20, spread=False):
                       ci.data_ptr(), cn.data_ptr(), cap)
     _lib.check(_lib.lib.ydbl_pred_candidates(pd, s))
     out = torch.zeros((B, 300, 6), device=dev); cnt = torch.zeros((B,), dtype=torch.int32, device=dev)
-    ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device=dev)  # zero-filled once (include/ydbl.h)
     nd = NmsDesc(cb.data_ptr(), cs.data_ptr(), cc.data_ptr(), ci.data_ptr(), cn.data_ptr(), B, cap, 0.7, 300, 30000, 0,
                  7680.0, 640.0, 640.0, out.data_ptr(), cnt.data_ptr(), ws.data_ptr())
     _lib.check(_lib.lib.ydbl_nms(nd, s))

@@ -56,7 +56,7 @@ print(f"largest image {i}: {cnt[i]} candidates, classes {np.bincount(cls[i, :cnt
 cap = sess.cand_score.shape[1]
 out = torch.zeros((B, 300, 6), device=dev)
 oc = torch.zeros((B,), dtype=torch.int32, device=dev)
-ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device=dev)
+ws = torch.zeros(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device=dev)  # zero-filled once (include/ydbl.h)
 nd = NmsDesc(sess.cand_box.data_ptr(), sess.cand_score.data_ptr(), sess.cand_cls.data_ptr(), sess.cand_idx.data_ptr(),
              sess.cand_count.data_ptr(), B, cap, 0.7, 300, 30000, 0, 7680.0, 640.0, 640.0, out.data_ptr(),
              oc.data_ptr(), ws.data_ptr())

@@ -406,7 +406,7 @@ def test_nms_paths_agree_on_model_candidates(golden_dir, monkeypatch, groups):
     torch.cuda.synchronize()
     assert int(sess.cand_count.max()) > 300  # clusters large enough for several rank blocks
     cap = sess.cand_score.shape[1]
-    ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device="cuda")
+    ws = torch.zeros(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device="cuda")  # zero-filled once (include/ydbl.h)
     outs = []
     for fast, per_image in (("1", 0), ("0", 0), ("1", 1)):  # per_image 1: the session's own schedule at conf .25
         monkeypatch.setenv("YDBL_NMS_FAST", fast)

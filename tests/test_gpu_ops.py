@@ -952,6 +952,17 @@ def _rand_pred(n, nc, A, seed, ties=False):
     dict(nc=1, A=1025, conf=0.0, iou=0.7, multi=False),
     dict(nc=3, A=1000, conf=0.0, iou=0.5, multi=False, max_nms=700),  # max_nms cut on the pair-matrix path
     dict(nc=2, A=960, conf=0.0, iou=0.7, multi=False, max_det=5),     # max_det inside the first rank block
+    # wide pair-matrix path (1024 < n <= 8192: ranks and rank-space rows on the chip, chunked sweep) and past it
+    dict(nc=1, A=1188, conf=0.0, iou=0.7, multi=False),             # DBL-s bs8's worst image size: 2 chunks
+    dict(nc=3, A=3000, conf=0.0, iou=0.6, multi=False, ties=True),  # 3000, equal scores: index order decides
+    dict(nc=1, A=6210, conf=0.0, iou=0.7, multi=False),             # DBL-l 1280's worst image size
+    dict(nc=1, A=8192, conf=0.0, iou=0.5, multi=False),             # the largest it takes
+    dict(nc=1, A=8193, conf=0.0, iou=0.5, multi=False),             # one more: sort + chunked sweep
+    dict(nc=1, A=6000, conf=0.0, iou=0.95, multi=False, max_det=3000),  # thousands of keeps over 6 chunks
+    dict(nc=2, A=3000, conf=0.0, iou=0.7, multi=True, max_nms=2500),    # max_nms cut on the wide path
+    dict(nc=1, A=2000, conf=0.0, iou=0.0, multi=False),             # iou 0 on the wide path
+    dict(nc=3, A=4000, conf=0.0, iou=0.7, multi=False, max_det=700),  # max_det reached in a later chunk
+    dict(nc=4, A=9000, conf=0.0, iou=0.7, multi=True),  # 36000 candidates > max_nms 30000: stable truncation
 ])
 @pytest.mark.parametrize("groups", ["1", "0"])
 @pytest.mark.parametrize("fast", ["1", "0"])

@@ -223,6 +223,10 @@ struct NmsArgs {
   int* gslot; uint64_t* gkey; int* gcount; int gk;  // per (image, class group) keep lists, gk entries each
   int cap;
   uint64_t* fmask; int* frank; int frows; int fast;  // pair-matrix path (nms_pair_kernel), frows rows per image
+  // wide pair-matrix path (NMS_FAST < n <= NMS_WIDE): per image wrows rows of rank accumulators (zero between
+  // calls: the sweep clears what nms_pair_kernel added), rank -> slot order, and the rank-space IoU rows
+  // (wwords words each; only the words at and right of a row's own 64-rank block are written)
+  unsigned long long* wacc; int* worder; uint64_t* wmask; int wrows; int wwords;
   double thr; int max_det, max_nms; float off_scale;
   float clip_w, clip_h;
   float* out; int* out_count;
@@ -344,6 +348,8 @@ __device__ __forceinline__ float rlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
+constexpr int NMS_WIDE = 8192;       // candidates per image on the wide pair-matrix path (rows in rank space)
+constexpr int NMS_WIDE_COLS = 1024;  // columns per rank item of nms_pair_kernel (4 waves x 256)
 constexpr int NMS_PAIR_MAXB = 1024;  // images per launch on the pair-matrix path (block offsets in LDS)
 constexpr int NMS_PAIR_WGS = 512;    // workgroups, each taking 64 x 64 blocks in turn
 
@@ -361,7 +367,8 @@ __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
       if (bb < nimg) {
         const int nn = min(p.ccount[bb], p.cap);
         const int nbb = (nn + 63) >> 6;
-        cnt = nn <= NMS_FAST ? nbb * nbb : 0;
+        cnt = nn <= NMS_FAST ? nbb * nbb
+              : (nn <= NMS_WIDE && p.wrows > 0 ? nbb * ((nn + NMS_WIDE_COLS - 1) / NMS_WIDE_COLS) : 0);
       }
       int incl = cnt;
 #pragma unroll
@@ -390,11 +397,49 @@ __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
     const int n = min(p.ccount[b], p.cap);
     const int nb = (n + 63) >> 6;
     const int t = g - s_pre[b];
-    const int bi = t / nb, bj = t - bi * nb;
     const float* cb = p.cbox + (int64_t)b * p.cap * 4;
     const float* sc = p.cscore + (int64_t)b * p.cap;
     const int* ix = p.cidx + (int64_t)b * p.cap;
     const int* cc = p.ccls + (int64_t)b * p.cap;
+    if (n > NMS_FAST) {
+      // wide image: a rank item = 64 candidates (rows) against NMS_WIDE_COLS columns, wave w taking 256 of them;
+      // the item adds its count of smaller keys and one contribution into the row's 64-bit accumulator, and the
+      // row's last contribution (all ng column groups in) knows the final rank = the stable-sort position and
+      // writes order[rank] = slot
+      const int ng = (n + NMS_WIDE_COLS - 1) / NMS_WIDE_COLS;
+      const int bi = t / ng, gq = t - bi * ng;
+      const int i = bi * 64 + lane, ic = min(i, n - 1);
+      const uint64_t ki = make_key(sc[ic], ix[ic]);
+      const int c0 = gq * NMS_WIDE_COLS + wave * 256;
+      uint32_t kh[4], kl[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // the wave's 256 column keys, all loads issued first
+        const int jc = min(c0 + q * 64 + lane, n - 1);
+        const uint64_t k = make_key(sc[jc], ix[jc]);
+        kh[q] = (uint32_t)(k >> 32);
+        kl[q] = (uint32_t)k;
+      }
+      int below = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int ns = min(64, n - (c0 + q * 64));  // wave-uniform; <= 0 past the end
+        for (int s = 0; s < ns; ++s) {
+          const uint64_t k = ((uint64_t)__builtin_amdgcn_readlane(kh[q], s) << 32) | __builtin_amdgcn_readlane(kl[q], s);
+          below += k < ki;
+        }
+      }
+      s_cnt[wave][lane] = below;
+      __syncthreads();
+      if (wave == 0 && i < n) {
+        const int tot = s_cnt[0][lane] + s_cnt[1][lane] + s_cnt[2][lane] + s_cnt[3][lane];
+        const unsigned long long old =
+            atomicAdd(p.wacc + (int64_t)b * p.wrows + i, (1ull << 32) | (unsigned long long)(unsigned)tot);
+        if ((int)(old >> 32) == ng - 1) p.worder[(int64_t)b * p.wrows + (int)(uint32_t)old + tot] = i;
+      }
+      __syncthreads();
+      continue;
+    }
+    const int bi = t / nb, bj = t - bi * nb;
     auto box_of = [&](int i) -> f32x4 {  // the sweep's class-offset box (nms_kernel load_box)
       const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)i * 4);
       const float c = float(cc[i]) * p.off_scale;
@@ -423,6 +468,74 @@ __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
       p.frank[((int64_t)b * NMS_FW + bj) * p.frows + i] = s_cnt[0][lane] + s_cnt[1][lane] + s_cnt[2][lane] + s_cnt[3][lane];
     }
     __syncthreads();
+  }
+}
+
+// Wide images, after nms_pair_kernel has ranked them: the IoU > thr bits of every pair of the first m = min(n,
+// max_nms) ranks, in rank space, row r word w bit s = IoU(rank r, rank 64w + s) > thr, for the 64 x 64 blocks on
+// and right of the diagonal (w >= r / 64; the sweep reads no other word).  Each wave takes one block at a time
+// (lane = row, the 64 columns broadcast by readlane), no barrier; persistent over all images' blocks.
+__global__ __launch_bounds__(256) void nms_wide_mask_kernel(NmsArgs p, int nimg) {
+  __shared__ int s_pre[NMS_PAIR_MAXB + 1];  // s_pre[b] = blocks of images < b
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (wave == 0) {
+    int run = 0;
+    for (int b0 = 0; b0 < nimg; b0 += 64) {
+      const int bb = b0 + lane;
+      int cnt = 0;
+      if (bb < nimg) {
+        const int nn = min(p.ccount[bb], p.cap);
+        const int nbm = (min(nn, p.max_nms) + 63) >> 6;
+        cnt = nn > NMS_FAST && nn <= NMS_WIDE ? nbm * (nbm + 1) / 2 : 0;
+      }
+      int incl = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      if (bb < nimg) s_pre[bb + 1] = run + incl;
+      run += __shfl(incl, 63);
+    }
+    if (lane == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+  const int total = s_pre[nimg];
+  for (int g = blockIdx.x * 4 + wave; g < total; g += gridDim.x * 4) {
+    int lo = 0, hi = nimg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_pre[mid] <= g) lo = mid;
+      else hi = mid - 1;
+    }
+    const int b = lo;
+    const int n = min(p.ccount[b], p.cap);
+    const int m = min(n, p.max_nms);
+    const int nbm = (m + 63) >> 6;
+    int t = g - s_pre[b], bi = 0;  // upper-triangular block index -> (bi, bj >= bi)
+    while (t >= nbm - bi) {
+      t -= nbm - bi;
+      ++bi;
+    }
+    const int bj = bi + t;
+    const float* cb = p.cbox + (int64_t)b * p.cap * 4;
+    const int* cc = p.ccls + (int64_t)b * p.cap;
+    const int* ord = p.worder + (int64_t)b * p.wrows;
+    const int r = bi * 64 + lane;
+    const int si = ord[min(r, m - 1)], sj = ord[min(bj * 64 + lane, m - 1)];
+    const f32x4 vi = *reinterpret_cast<const f32x4*>(cb + (int64_t)si * 4);
+    const f32x4 vj = *reinterpret_cast<const f32x4*>(cb + (int64_t)sj * 4);
+    const float ci = float(cc[si]) * p.off_scale, cj = float(cc[sj]) * p.off_scale;
+    const f32x4 xi = f32x4{vi[0] + ci, vi[1] + ci, vi[2] + ci, vi[3] + ci};
+    const f32x4 xj = f32x4{vj[0] + cj, vj[1] + cj, vj[2] + cj, vj[3] + cj};
+    const float ai = (xi[2] - xi[0]) * (xi[3] - xi[1]);
+    const int ns = min(64, m - bj * 64);
+    uint64_t bits = 0;
+    for (int s = 0; s < ns; ++s) {
+      const f32x4 y = f32x4{rlane(xj[0], s), rlane(xj[1], s), rlane(xj[2], s), rlane(xj[3], s)};
+      if (iou_gt(xi, ai, y, p.thr)) bits |= 1ull << s;
+    }
+    if (r < m) p.wmask[((int64_t)b * p.wrows + r) * p.wwords + bj] = bits;
   }
 }
 
@@ -455,6 +568,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   constexpr int LDS_BOXES = NMS_SORT_LDS * 8 / 16;
 
   NMS_STAMP(0, __builtin_amdgcn_s_memrealtime());
+  bool kept_rank = false;  // the wide path keeps ranks in kept_slot (slot = worder[rank])
   const int b = GROUPS ? blockIdx.x / NMS_GROUPS : blockIdx.x;
   const int grp = GROUPS ? blockIdx.x % NMS_GROUPS : 0;
   int n = min(p.ccount[b], p.cap);
@@ -573,6 +687,153 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     __syncthreads();
     NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
     NMS_STAMP(5, 0ull);
+  } else if (p.fast && p.wrows > 0 && n <= NMS_WIDE) {
+    // ---- wide pair-matrix path: the ranks and rank-space IoU rows come from nms_pair_kernel and
+    // nms_wide_mask_kernel; the sweep walks the ranks in chunks of NMS_FAST.  Per chunk: the ranks not yet
+    // removed by an earlier chunk's kept rows are compacted (rank order kept), their rows' words over the chunk
+    // are staged in LDS and the chunk runs exactly the pair-matrix sweep above (within-block words, fixed-point
+    // block greedy, kept rows ORed into the chunk's removed flags); then the rows of the chunk's new keeps are
+    // ORed, over the ranks right of the chunk, into the image's removed bits -- so a chunk only ever sweeps
+    // ranks nothing kept before it suppresses.
+    if constexpr (GROUPS) {
+      if (grp != 0) {  // the whole image is group 0's
+        if (threadIdx.x == 0) p.gcount[(int64_t)b * NMS_GROUPS + grp] = 0;
+        return;
+      }
+    }
+    kept_rank = true;
+    const int m = min(n, p.max_nms);
+    const int W = (m + 63) >> 6;
+    uint64_t* wrem = reinterpret_cast<uint64_t*>(chunk_box);  // removed bits of ranks 0 .. NMS_WIDE - 1
+    static_assert(sizeof(chunk_box) >= NMS_WIDE / 8, "wide removed bits alias chunk_box");
+    for (int w = threadIdx.x; w < NMS_WIDE / 64; w += NMS_THREADS) wrem[w] = 0ull;
+    unsigned long long* acc = p.wacc + (int64_t)b * p.wrows;
+    for (int i = threadIdx.x; i < n; i += NMS_THREADS) acc[i] = 0ull;  // ready for the next call (pair kernel done)
+    const uint64_t* gm = p.wmask + (int64_t)b * p.wrows * p.wwords;
+    uint64_t* smask = reinterpret_cast<uint64_t*>(s_raw);  // [compact position][NMS_FW], mslot order
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    if (t == 0) s_nk = 0;
+    __syncthreads();
+    for (int R0 = 0; R0 < m; R0 += NMS_FAST) {
+      const int nk_prev = s_nk;
+      if (nk_prev >= p.max_det) break;
+      const int L = min(NMS_FAST, m - R0);
+      // (a) compaction of the chunk's live ranks: s_order[pos] = local rank (0 .. L-1)
+      const int r = R0 + t;
+      const bool alive = t < L && !((wrem[r >> 6] >> (r & 63)) & 1ull);
+      const uint64_t bal = __ballot(alive);
+      if (lane == 0) s_wsum[wave] = __popcll(bal);
+      __syncthreads();
+      int off = 0, cnt = 0;
+#pragma unroll
+      for (int w = 0; w < NMS_THREADS / 64; ++w) {
+        const int v = s_wsum[w];
+        off += w < wave ? v : 0;
+        cnt += v;
+      }
+      if (alive) s_order[off + __popcll(bal & ((1ull << lane) - 1))] = t;
+      __syncthreads();
+      if (cnt == 0) continue;
+      // (b) rows of the live ranks, words of this chunk (words left of a row's own block were not written: 0)
+      const int w0 = R0 >> 6, nbw = (L + 63) >> 6;
+      {
+        uint64_t v[NMS_FW];
+#pragma unroll
+        for (int k = 0; k < NMS_FW; ++k) {
+          const int e = t + k * NMS_THREADS, pos = e >> 4, w = e & (NMS_FW - 1);
+          v[k] = 0ull;
+          if (pos < cnt && w < nbw) {
+            const int rr = R0 + s_order[pos];
+            if (w0 + w >= (rr >> 6)) v[k] = gm[(int64_t)rr * p.wwords + w0 + w];
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < NMS_FW; ++k) {
+          const int e = t + k * NMS_THREADS;
+          if ((e >> 4) < cnt) smask[mslot(e >> 4, e & (NMS_FW - 1))] = v[k];
+        }
+      }
+      __syncthreads();
+      // (c) within-block words over compact positions (columns: local ranks)
+      if ((t & ~63) < cnt) {
+        const int k0 = t & ~63, rl = t & 63;
+        const int cr = t < cnt ? s_order[t] : 0;
+        const int send = min(64, cnt - k0);
+        uint64_t dw = 0;
+#pragma unroll 8
+        for (int q = 0; q < 64; ++q) {
+          const int cq = __builtin_amdgcn_readlane(cr, q);
+          const uint64_t bit = (smask[mslot(t, (cq >> 6) & (NMS_FW - 1))] >> (cq & 63)) & 1ull;
+          dw |= (q > rl && q < send) ? bit << q : 0ull;
+        }
+        if (t < cnt) s_dw[t] = dw;
+      }
+      __syncthreads();
+      // (d) the sweep of the pair-matrix path over the compact positions
+      if (t < 64) {
+        uint64_t rem = 0;  // lane w < nbw: removed flags of local ranks 64w .. 64w+63
+        int nk = nk_prev;
+        for (int t0 = 0; t0 < cnt && nk < p.max_det; t0 += 64) {
+          const bool valid = t0 + lane < cnt;
+          const int myc = valid ? s_order[t0 + lane] : 0;
+          const uint64_t dw = valid ? s_dw[t0 + lane] : 0ull;
+          const int wsrc = myc >> 6;
+          const uint32_t rlo = __shfl((uint32_t)rem, wsrc), rhi = __shfl((uint32_t)(rem >> 32), wsrc);
+          const uint64_t rw = ((uint64_t)rhi << 32) | rlo;
+          const uint64_t M = __ballot(valid && !((rw >> (myc & 63)) & 1));
+          const int nk0 = nk;
+          uint64_t K = M;
+          for (;;) {
+            const uint64_t Wo = __ockl_wfred_or_u64((K >> lane) & 1 ? dw : 0ull);
+            const uint64_t Kn = M & ~Wo;
+            if (Kn == K) break;
+            K = Kn;
+          }
+          for (int extra = __popcll(K) - (p.max_det - nk0); extra > 0; --extra) K &= ~(1ull << (63 - __clzll(K)));
+          nk = nk0 + __popcll(K);
+          if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = R0 + myc;  // a rank here
+          while (K) {
+            int c[8];
+            bool ok[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const int tt = __ffsll((long long)K) - 1;
+              K &= K - 1;
+              ok[q] = tt >= 0;
+              c[q] = t0 + (tt & 63);  // the kept candidate's compact position = its staged row
+            }
+            uint64_t row[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) row[q] = smask[mslot(c[q], lane & (NMS_FW - 1))];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) rem |= ok[q] && lane < nbw ? row[q] : 0ull;
+          }
+        }
+        if (lane == 0) s_nk = nk;
+      }
+      __syncthreads();
+      // (e) the new keeps' rows, right of the chunk, into the image's removed bits (8 loads in flight per thread)
+      const int nk_now = s_nk, wbeg = w0 + NMS_FW;
+      if (nk_now < p.max_det && wbeg < W && nk_now > nk_prev) {
+        const int span = W - wbeg, tot = (nk_now - nk_prev) * span;
+        for (int e0 = t; e0 < tot; e0 += 8 * NMS_THREADS) {
+          uint64_t v[8];
+          int wd[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int e = e0 + q * NMS_THREADS;
+            const int k = e / span, w = wbeg + (e - k * span);
+            wd[q] = e < tot ? w : -1;
+            v[q] = e < tot ? gm[(int64_t)kept_slot[nk_prev + k] * p.wwords + w] : 0ull;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            if (wd[q] >= 0 && v[q]) atomicOr(reinterpret_cast<unsigned long long*>(&wrem[wd[q]]), (unsigned long long)v[q]);
+        }
+      }
+      __syncthreads();
+    }
+    NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
   } else {
     bool listed = false;  // GROUPS: this group's (key, slot) list is already in s_keys / s_vals
     if constexpr (GROUPS) {
@@ -845,7 +1106,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   if constexpr (GROUPS) {  // this group's keep list for nms_merge_kernel
     const int64_t gi = (int64_t)b * NMS_GROUPS + grp;
     for (int k = threadIdx.x; k < kept; k += NMS_THREADS) {
-      const int slot = kept_slot[k];
+      const int slot = kept_rank ? p.worder[(int64_t)b * p.wrows + kept_slot[k]] : kept_slot[k];
       const int64_t o = (int64_t)b * p.cap + slot;
       p.gslot[gi * p.gk + k] = slot;
       p.gkey[gi * p.gk + k] = make_key(p.cscore[o], p.cidx[o]);
@@ -854,7 +1115,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
     return;
   }
   for (int k = threadIdx.x; k < kept; k += NMS_THREADS) {
-    const int slot = kept_slot[k];
+    const int slot = kept_rank ? p.worder[(int64_t)b * p.wrows + kept_slot[k]] : kept_slot[k];
     const int64_t o = (int64_t)b * p.cap + slot;
     f32x4 v = *reinterpret_cast<const f32x4*>(p.cbox + o * 4);
     if (p.clip_w > 0.f) {
@@ -1027,6 +1288,8 @@ static int64_t nms_sort_len(int32_t cap) { return cap <= NMS_SORT_LDS ? 0 : next
 static int32_t nms_group_len(int32_t cap) { return cap < NMS_MAX_DET ? cap : NMS_MAX_DET; }
 // rows per image of the pair-matrix workspace: candidates up to NMS_FAST, in whole 64-row blocks
 static int32_t nms_fast_rows(int32_t cap) { return (std::min(cap, NMS_FAST) + 63) / 64 * 64; }
+// rows per image of the wide path (0: cap <= NMS_FAST, no image can be wide)
+static int32_t nms_wide_rows(int32_t cap) { return cap <= NMS_FAST ? 0 : (std::min(cap, NMS_WIDE) + 63) / 64 * 64; }
 
 #ifdef YDBL_NMS_STAMPS
 extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
@@ -1037,9 +1300,11 @@ extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
 extern "C" int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms) {
   (void)max_nms;
   if (n < 1 || cap < 1) return 16;
-  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap), R = nms_fast_rows(cap);
+  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap), R = nms_fast_rows(cap), RW = nms_wide_rows(cap);
   // + pair-matrix rows (u64 x NMS_FW) and partial ranks (int x NMS_FW) per candidate row, 8-byte aligned
-  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 8 + (int64_t)n * R * NMS_FW * 12 + 16;
+  // + wide rows: rank accumulator (u64), order (int), IoU row (RW / 64 u64) per row
+  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 8 + (int64_t)n * R * NMS_FW * 12 + 16 +
+         (int64_t)n * RW * (12 + RW / 8) + 16;
 }
 
 extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
@@ -1074,9 +1339,20 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   a.frows = nms_fast_rows(d->cap);
   a.fmask = reinterpret_cast<uint64_t*>(a.gcount + (int64_t)d->n * NMS_GROUPS + ((int64_t)d->n * NMS_GROUPS & 1));
   a.frank = reinterpret_cast<int*>(a.fmask + (int64_t)d->n * a.frows * NMS_FW);
+  a.wrows = nms_wide_rows(d->cap);
+  a.wwords = a.wrows / 64;
+  {
+    const int64_t fr = (int64_t)d->n * NMS_FW * a.frows;  // ints of frank, then 8-byte alignment
+    a.wacc = reinterpret_cast<unsigned long long*>(a.frank + fr + (fr & 1));
+    a.wmask = reinterpret_cast<uint64_t*>(a.wacc + (int64_t)d->n * a.wrows);
+    a.worder = reinterpret_cast<int*>(a.wmask + (int64_t)d->n * a.wrows * a.wwords);
+  }
+  const char* we = getenv("YDBL_NMS_WIDE");  // A/B switch (read per launch: tests): 0 = no wide pair-matrix path
+  if (we && *we == '0') a.wrows = 0;
   const char* fe = getenv("YDBL_NMS_FAST");  // A/B switch (read per launch: tests): 0 = sort + chunked sweep only
   a.fast = !(fe && *fe == '0') && d->n <= NMS_PAIR_MAXB;
   if (a.fast) nms_pair_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
+  if (a.fast && a.wrows > 0) nms_wide_mask_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
   // class-split sweep + merge (non-agnostic); the one-workgroup-per-image form for agnostic NMS or on request
   const char* ev = getenv("YDBL_NMS_GROUPS");  // A/B switch (read per launch: tests): 0 = one workgroup per image
   if (d->agnostic || d->per_image || (ev && *ev == '0')) {

@@ -152,7 +152,7 @@ class DetectSession:
             self.pred = torch.empty((batch, 4 + nc, A), dtype=torch.float32, device=dev) if keep_pred else None
             self.det, self.count, self.out_flat = _det_count(batch, self.max_det, dev)
         self.classes_t = (torch.tensor(list(classes), dtype=torch.int32, device=dev) if classes is not None else None)
-        ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(batch, cap, max_nms)), dtype=torch.uint8, device=dev)
+        ws = torch.zeros(int(_lib.lib.ydbl_nms_workspace(batch, cap, max_nms)), dtype=torch.uint8, device=dev)  # zero-filled once (include/ydbl.h)
         plan.buffers += [self.cand_box, self.cand_score, self.cand_cls, self.cand_idx, self.cand_count, self.det,
                          self.count, ws]
         boxes = (View * 3)(*[lv.cslice(0, 64).struct() for lv in cm.levels])

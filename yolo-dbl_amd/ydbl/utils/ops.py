@@ -97,7 +97,7 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
     _lib.check(_lib.lib.ydbl_pred_candidates(pd, stream), "ydbl_pred_candidates")
     out = torch.zeros((bs, max_det, 6), dtype=torch.float32, device=dev)
     cnt = torch.zeros((bs,), dtype=torch.int32, device=dev)
-    ws = torch.empty(int(_lib.lib.ydbl_nms_workspace(bs, cap, max_nms)), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(int(_lib.lib.ydbl_nms_workspace(bs, cap, max_nms)), dtype=torch.uint8, device=dev)  # zero-filled once (include/ydbl.h)
     nd = NmsDesc(cand_box.data_ptr(), cand_score.data_ptr(), cand_cls.data_ptr(), cand_idx.data_ptr(),
                  cand_count.data_ptr(), bs, cap, float(iou_thres), int(max_det), int(max_nms), int(bool(agnostic)),
                  float(max_wh), 0.0, 0.0, out.data_ptr(), cnt.data_ptr(), ws.data_ptr())
