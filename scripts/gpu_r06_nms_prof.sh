@@ -7,3 +7,4 @@ for c in 0 3 6; do
       > $T/p$c.log 2>&1 || exit 1
   python scripts/rocpd_stats.py $T/p$c/run_results.db > $T/case${c}_kernel_stats.csv || exit 1
 done
+timeout -k 10 120 python -u scripts/nms_wide_stamps.py > $T/stamps.txt 2>&1

@@ -1,7 +1,7 @@
-"""Round 6: time ydbl_nms alone (HIP events over back-to-back launches) with the wide pair-matrix path on and off
-(YDBL_NMS_WIDE, read per launch), per-image and class-split schedules, on synthetic candidate sets shaped like
-the configs' worst images: DBL-s 640 bs4 sub-batch (1188 candidates), DBL-l 1280 bs4 (6210 of 33600 anchors),
-DBL-n bs16 control (<= 1024: the pair-matrix path, unchanged).
+"""Round 6: time ydbl_nms alone (HIP events over back-to-back launches): the rank-space pair-matrix path (images
+<= 8192 candidates) against the sort + chunked sweep (YDBL_NMS_FAST=0, read per launch), per-image and class-split
+schedules, on synthetic candidate sets shaped like the configs' worst images: DBL-s 640 bs4 sub-batch (1188
+candidates), DBL-l 1280 bs4 (6210 of 33600 anchors), DBL-n bs16 (<= 645, the bench).
 
     python scripts/nms_wide_bench.py
 """
@@ -45,7 +45,7 @@ def run(counts, nc, A, size, per_image, reps=20):
     _lib.check(_lib.lib.ydbl_pred_candidates(pd, s))
     res = {}
     for wide in ("1", "0"):
-        os.environ["YDBL_NMS_WIDE"] = wide
+        os.environ["YDBL_NMS_FAST"] = wide
         out = torch.zeros((B, 300, 6), device=dev); cnt = torch.zeros((B,), dtype=torch.int32, device=dev)
         ws = torch.zeros(int(_lib.lib.ydbl_nms_workspace(B, cap, 30000)), dtype=torch.uint8, device=dev)
         nd = NmsDesc(cb.data_ptr(), cs.data_ptr(), cc.data_ptr(), ci.data_ptr(), cn.data_ptr(), B, cap, 0.7, 300,
@@ -64,7 +64,7 @@ def run(counts, nc, A, size, per_image, reps=20):
             torch.cuda.synchronize()
             best = min(best, a.elapsed_time(b) / reps * 1e3)
         res[wide] = (best, out.clone(), cnt.clone(), cn.tolist())
-    os.environ.pop("YDBL_NMS_WIDE")
+    os.environ.pop("YDBL_NMS_FAST")
     same = torch.equal(res["1"][1], res["0"][1]) and torch.equal(res["1"][2], res["0"][2])
     return res["1"][0], res["0"][0], same, res["1"][3], res["1"][2].tolist()
 
@@ -75,10 +75,10 @@ cases = [("DBL-s bs4: 1188,900,700,500", [1188, 900, 700, 500], 3, 8400, 640),
          ("DBL-l bs4: 6210,4000,3000,2000", [6210, 4000, 3000, 2000], 3, 33600, 1280),
          ("4 x 6210", [6210] * 4, 3, 33600, 1280),
          ("1 x 8192", [8192], 1, 33600, 1280),
-         ("DBL-n bs16 control: 16 x 640", [640] * 16, 3, 8400, 640)]
+         ("DBL-n bs16: 16 x 640", [640] * 16, 3, 8400, 640)]
 if len(sys.argv) > 1:  # one case under a profiler: python scripts/nms_wide_bench.py <case> <per_image> <wide>
     label, counts, nc, A, size = cases[int(sys.argv[1])]
-    os.environ["YDBL_NMS_WIDE"] = sys.argv[3]
+    os.environ["YDBL_NMS_FAST"] = sys.argv[3]
     B = len(counts)
     p = pred(B, nc, A, counts, size).float().contiguous()
     cb = torch.empty((B, A, 4), device="cuda"); cs = torch.empty((B, A), device="cuda")
@@ -100,5 +100,5 @@ if len(sys.argv) > 1:  # one case under a profiler: python scripts/nms_wide_benc
 for label, counts, nc, A, size in cases:
     for per_image in (1, 0):
         w, o, same, n, kept = run(counts, nc, A, size, per_image)
-        print(f"{label:32s} per_image {per_image}: wide {w:7.1f} us   sort path {o:7.1f} us   bit-equal {same}   "
+        print(f"{label:32s} per_image {per_image}: pair-matrix {w:7.1f} us   sort path {o:7.1f} us   bit-equal {same}   "
               f"cands {n}  kept {kept}", flush=True)

@@ -73,6 +73,10 @@ FP32_FACTOR = {"n": (2.0, 2.0), "s": (2.5, 2.0), "l": (2.0, 2.0), "x": (2.0, 3.0
 # NMS decisions within the tolerance of flipping, beyond twice the reference fp32 path's own count (a count of rare
 # events; measured round 5: s640 bs32 one graph 2, every other fixture / layout 0 beyond the reference's)
 FP32_BORDERLINE_EXTRA = {"n": 0, "s": 2, "l": 0, "x": 0}
+# fp16: final detections whose NMS decision lies within the fp16 tolerance of flipping ("borderline") may number at
+# most the reference half path's own count on the fixture + this margin (round 5 measured, every layout: n640 7-12
+# against the half path's 35, s640 45-47 against 58, l1280 17-21 against 18, x640 0 against 0)
+FP16_BORDERLINE_EXTRA = {"n": 3, "s": 3, "l": 6, "x": 3}
 
 
 def fp32_rule_max(st, scale):

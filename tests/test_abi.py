@@ -99,14 +99,10 @@ def test_workspace_queries():
     from ydbl import _lib
 
     # global sort scratch (cap > 8192: next pow2 x (8 B key + 4 B slot)) + class-group keep lists
-    # (8 groups x min(cap, 4096) x (8 B key + 4 B slot) + a 4 B count each) + 16
-    # sort scratch + class-group keep lists + pair-matrix rows / partial ranks (16 words per row, <= 1024 rows)
-    # + wide rows (cap > 1024: min(cap, 8192) rows of an 8 B rank accumulator, a 4 B order entry and a
-    # min(cap, 8192) / 8 B IoU row)
+    # (8 groups x min(cap, 4096) x (8 B key + 4 B slot) + a 4 B count each) + 8 + pair-matrix rows: min(cap, 8192)
+    # rounded to 64 per image, each an 8 B rank accumulator, a 4 B order entry and a rows / 8 B IoU row, + 16
     assert _lib.lib.ydbl_nms_workspace(2, 8400, 30000) == (2 * 16384 * 12 + 2 * 8 * (4096 * 12 + 4) + 8
-                                                           + 2 * 1024 * 16 * 12 + 16 + 2 * 8192 * (12 + 1024) + 16)
-    assert _lib.lib.ydbl_nms_workspace(3, 100, 30000) == 3 * 8 * (100 * 12 + 4) + 8 + 3 * 128 * 16 * 12 + 16 + 16
-    assert _lib.lib.ydbl_nms_workspace(1, 1188, 30000) - _lib.lib.ydbl_nms_workspace(1, 1024, 30000) == (
-        1216 * (12 + 1216 // 8) + 8 * (1188 - 1024) * 12)
+                                                           + 2 * 8192 * (12 + 1024) + 16)
+    assert _lib.lib.ydbl_nms_workspace(3, 100, 30000) == 3 * 8 * (100 * 12 + 4) + 8 + 3 * 128 * (12 + 16) + 16
     assert _lib.lib.ydbl_lsk_gate_workspace(2, 20, 20) == 2 * 400 * 2 * 4
     assert _lib.lib.ydbl_hg_workspace(1, 1600, 64, 4) > 0

@@ -25,7 +25,7 @@ import pytest
 import torch
 
 from parity_util import (batch_images, build_pair, class_agreement, detections, direct_report, err_stats, fp16_rule, fp32_rule,
-                         fp32_rule_max, FP32_BORDERLINE_EXTRA, fp8_emulated_leg, gpu_pred, load_e2e, match_detections, ROLE_FX)
+                         fp32_rule_max, FP16_BORDERLINE_EXTRA, FP32_BORDERLINE_EXTRA, fp8_emulated_leg, gpu_pred, load_e2e, match_detections, ROLE_FX)
 
 pytestmark = pytest.mark.gpu
 
@@ -139,8 +139,12 @@ def test_e2e_fp16(golden_dir, name, batch, streams):
     assert bad == 0, (checked, bad)
     m = match_detections(ref_dets, dets, y64, meta["conf"], meta["iou"], tb, tc)
     print(f"   detections: {m['pairs']} pairs, {m['borderline']} borderline, {len(m['mismatches'])} mismatches "
-          f"(ref half path: {o16['det_mismatches']})")
+          f"(ref half path: {o16['det_borderline']} borderline, {o16['det_mismatches']} mismatches)")
     assert len(m["mismatches"]) <= 2 * o16["det_mismatches"] + 2, m["mismatches"][:5]
+    # borderline decisions bounded too, so a drift in them cannot pass silently: at most the half path's own count
+    # + the measured per-fixture margin (parity_util.FP16_BORDERLINE_EXTRA)
+    nb = o16["det_borderline"] + FP16_BORDERLINE_EXTRA[meta["scale"]]
+    assert m["borderline"] <= nb and m["pairs"] >= sum(len(d) for d in ref_dets) - nb - 2 * o16["det_mismatches"] - 2, m
 
 
 @pytest.mark.parametrize("fraction", [0.1, 0.25, 1.0])

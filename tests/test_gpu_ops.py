@@ -968,9 +968,9 @@ def _rand_pred(n, nc, A, seed, ties=False):
 @pytest.mark.parametrize("fast", ["1", "0"])
 def test_nms_bit_exact(case, groups, fast, monkeypatch):
     """groups "1": the class-split sweep (8 class-group workgroups per image + merge), "0": one workgroup
-    per image; fast "1": images with <= 1024 candidates take the pair-matrix path (nms_pair_kernel + the
-    rank-order sweep), "0": sort + chunked sweep for every image.  All bit-exact against the restated
-    torchvision semantics."""
+    per image; fast "1": images with <= 8192 candidates take the pair-matrix path (chip-wide ranks and
+    rank-space IoU rows, nms_pair_kernel + nms_mask_kernel, then the chunked rank-order sweep), "0": sort +
+    chunked sweep for every image.  All bit-exact against the restated torchvision semantics."""
     from oracle.ops import non_max_suppression as ref_nms
     from ydbl.utils.ops import non_max_suppression
 

@@ -5,13 +5,15 @@
 //          a per-image atomic counter; candidate order is irrelevant because NMS sorts by
 //          (score desc, original index asc), which is exactly the order torchvision's stable sort
 //          gives the reference (anchor order, or torch.where's (anchor, class) row-major order).
-// nms    : per-image bitonic key/value sort (LDS chunks of 4096 + global merge steps), then one
-//          1024-thread workgroup per image runs the greedy sweep with the suppression flags and
-//          the first 4096 sorted boxes in LDS.  The sweep stops after max_det keeps, which is the
-//          same as the reference's keep[:max_det] because keeps are produced in score order.
+// nms    : images with <= 8192 candidates: chip-wide ranks (= the stable sort's positions) and rank-space
+//          IoU > thr bit rows, then one 1024-thread workgroup per image sweeps 64-rank blocks (the pair-matrix
+//          path below); larger images: per-image bitonic key/value sort and a chunked greedy sweep with the
+//          suppression flags and the first 4096 sorted boxes in LDS.  Both stop after max_det keeps, which is
+//          the reference's keep[:max_det] because keeps are produced in score order.
 #include <stdlib.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include "common.hpp"
 
@@ -217,17 +219,20 @@ __device__ __forceinline__ uint64_t make_key(float score, int idx) {
 
 constexpr int NMS_GROUPS = 8;  // class groups (cls % 8) swept by separate workgroups
 
+struct IouT {  // iou_gt's fp32 thresholds (below)
+  float a, hi, lo;  // a = round-down(thr); hi / lo = a (1 +- 2e-5) +- 1e-30
+};
+
 struct NmsArgs {
   const float* cbox; const float* cscore; const int* ccls; const int* cidx; const int* ccount;
   uint64_t* gkeys; int* gvals; int L;  // global sort scratch (only when cap > NMS_SORT_LDS)
   int* gslot; uint64_t* gkey; int* gcount; int gk;  // per (image, class group) keep lists, gk entries each
   int cap;
-  uint64_t* fmask; int* frank; int frows; int fast;  // pair-matrix path (nms_pair_kernel), frows rows per image
-  // wide pair-matrix path (NMS_FAST < n <= NMS_WIDE): per image wrows rows of rank accumulators (zero between
-  // calls: the sweep clears what nms_pair_kernel added), rank -> slot order, and the rank-space IoU rows
-  // (wwords words each; only the words at and right of a row's own 64-rank block are written)
+  int fast;  // pair-matrix path (n <= NMS_WIDE): per image wrows rows of rank accumulators (zero between calls:
+  // the sweep clears what nms_pair_kernel added), rank -> slot order, and the rank-space IoU rows (wwords words
+  // each; only the words at and right of a row's own 64-rank block are written)
   unsigned long long* wacc; int* worder; uint64_t* wmask; int wrows; int wwords;
-  double thr; int max_det, max_nms; float off_scale;
+  double thr; IouT th; int max_det, max_nms; float off_scale;
   float clip_w, clip_h;
   float* out; int* out_count;
   int64_t ostride; int64_t cstride;  // floats per image of out, int32s per image of out_count
@@ -292,23 +297,25 @@ __device__ void reg_bitonic(uint64_t& key, int& val, int P, uint64_t* xk, int* x
   }
 }
 
-__device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4& b, double thr) {
+// torchvision's decision (double)(inter / uni) > thr, for the fp32 quotient q = inter / uni, is q > a with a the
+// largest float <= thr (q > a means q >= the next float, which is > thr; q <= a <= thr is not), so every compare
+// here is fp32.  inter * rcp(uni) is within a few ulp of q: it decides alone unless it lies within 2e-5
+// (relative) of a; only those cases pay for the IEEE division.  (IouT: set on the host by iou_thresholds.)
+__device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4& b, float area_b, const IouT& t) {
   const float xx1 = fmaxf(a[0], b[0]), yy1 = fmaxf(a[1], b[1]);
   const float xx2 = fminf(a[2], b[2]), yy2 = fminf(a[3], b[3]);
   const float ww = fmaxf(0.f, xx2 - xx1), hh = fmaxf(0.f, yy2 - yy1);
   const float inter = ww * hh;
   if (!(inter > 0.f)) return false;  // IoU 0 is never > thr (thr in [0, 1])
-  const float area_b = (b[2] - b[0]) * (b[3] - b[1]);
   const float uni = (area_a + area_b) - inter;
-  // The decision is torchvision's: the correctly rounded fp32 quotient inter / uni, compared in
-  // double.  inter * rcp(uni) is within a few ulp of that quotient, so it decides alone unless it
-  // lies within 1e-5 (relative) of the threshold; only those cases pay for the IEEE division.
   const float approx = inter * __builtin_amdgcn_rcpf(uni);
-  const double ad = (double)approx;
-  if (ad > thr * (1.0 + 1e-5) + 1e-30) return true;
-  if (ad < thr * (1.0 - 1e-5) - 1e-30) return false;
-  const float ovr = inter / uni;
-  return (double)ovr > thr;
+  if (approx > t.hi) return true;
+  if (approx < t.lo) return false;
+  return inter / uni > t.a;
+}
+
+__device__ __forceinline__ bool iou_gt(const f32x4& a, float area_a, const f32x4& b, const IouT& t) {
+  return iou_gt(a, area_a, b, (b[2] - b[0]) * (b[3] - b[1]), t);
 }
 
 // Diagnostic build only (-DYDBL_NMS_STAMPS, scripts/build_stamps.sh detect, scripts/nms_stamps.py): per-workgroup phase timestamps.
@@ -323,52 +330,46 @@ __device__ unsigned long long g_nms_stamps[16 * 4096];
 #define NMS_TICK(acc) do { } while (0)
 #endif
 
-// ---- pair-matrix path for images with n <= NMS_FAST candidates (the common case) --------------------
-// The greedy sweep of one image is serial, but everything it consumes is not: nms_pair_kernel spreads the
-// n x n candidate pairs of every image over the chip (64 x 64 blocks, one per workgroup at a time, each
-// wave testing 16 of the block's columns) and writes, in candidate (slot) order,
-//   fmask[b][i][w] bit s = IoU(box i, box 64w+s) > thr   (torchvision's decision, iou_gt; the IoU is
-//                                                         symmetric bit for bit, so row i is what box i
-//                                                         suppresses whichever of the two ranks first)
-//   frank[b][w][i]       = #{j in block w : key_j < key_i} (partial ranks; keys are unique)
-// and nms_kernel then only sums the ranks (rank = sort position, as the stable sort), stages the rows in
-// LDS and runs the sweep in rank order on one wave, 64 ranks at a time: a candidate is kept iff its bit
-// in the running removed mask is clear and no kept candidate earlier in its block suppresses it, and a
-// kept candidate ORs its row into the mask.  Rows of candidates ranked earlier get bits set too, which
-// changes nothing: their decision is already made.
-constexpr int NMS_FAST = 1024;        // candidates per image on this path (mask rows staged in LDS: 128 KiB)
-constexpr int NMS_FW = NMS_FAST / 64;  // 64-bit words per mask row
+// ---- pair-matrix path for images with n <= NMS_WIDE candidates (every predict image) -------------------
+// The greedy sweep of one image is serial, but everything it consumes is not.  Two chip-wide kernels prepare it:
+//   nms_pair_kernel  ranks every candidate: its count of smaller sort keys (keys are unique: they carry the
+//                    original index) = its position in the reference's stable descending sort, summed over
+//                    column groups in a 64-bit accumulator whose last contribution writes order[rank] = slot;
+//   nms_mask_kernel  writes, in RANK space, row r word w bit s = IoU(rank r, rank 64w+s) > thr (torchvision's
+//                    decision, iou_gt) for the 64 x 64 blocks on and right of the diagonal (rows of
+//                    ceil(m / 64) words, packed per image).
+// nms_kernel then sweeps the ranks in chunks of NMS_FAST: the chunk's rows are staged in LDS, and one wave walks
+// its 64-rank blocks in order -- a block is one mask word, so its live mask is ~(removed word) and its within-
+// block suppression words are the rows' diagonal words: a candidate is kept iff it is live and no kept
+// candidate earlier in its block suppresses it (the block greedy as the fixed point of K' = live & ~OR_{s in K}
+// D[s], one DPP wave-OR per step), and kept rows are ORed into the removed words.  Between chunks the new keeps'
+// rows are ORed, over the later ranks, into the image's removed bits.  Rows of earlier ranks would only set bits
+// whose decision is already made.
+constexpr int NMS_FAST = 1024;        // ranks per sweep chunk (rows staged in LDS: 128 KiB)
+constexpr int NMS_FW = NMS_FAST / 64;  // 64-bit words per staged row
+constexpr int NMS_WIDE = 8192;         // candidates per image on this path (rank-space rows of 1 KiB)
+constexpr int NMS_RANK_COLS = 1024;    // columns per rank item of nms_pair_kernel (4 waves x 256)
 
-// LDS slot of word w of mask row c: the words of a row are XOR-permuted by the row's low bits, so that
-// 64 lanes reading the same word of 64 different rows (the rank-word build) spread over the banks, while
+// LDS slot of word w of staged row c: the words of a row are XOR-permuted by the row's low bits, so that
+// 64 lanes reading the same word of 64 different rows (the diagonal-word reads) spread over the banks, while
 // the 16 words of one row (the sweep's row reads) stay one conflict-free 128-byte line.
 __device__ __forceinline__ int mslot(int c, int w) { return c * NMS_FW + (w ^ (c & (NMS_FW - 1))); }
 
-__device__ __forceinline__ float rlane(float v, int l) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
-}
-
-constexpr int NMS_WIDE = 8192;       // candidates per image on the wide pair-matrix path (rows in rank space)
-constexpr int NMS_WIDE_COLS = 1024;  // columns per rank item of nms_pair_kernel (4 waves x 256)
 constexpr int NMS_PAIR_MAXB = 1024;  // images per launch on the pair-matrix path (block offsets in LDS)
-constexpr int NMS_PAIR_WGS = 512;    // workgroups, each taking 64 x 64 blocks in turn
+constexpr int NMS_PAIR_WGS = 512;    // workgroups of the two persistent chip-wide kernels
 
-// Persistent over all images' blocks: no workgroup is launched for an image with few candidates (a
-// (32 x images) grid of one block per wave took 22 us, mostly dispatching empty workgroups and walking a
-// block's 64 columns on one wave), and the blocks of a heavy image spread over the whole chip.
-__global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
-  __shared__ int s_pre[NMS_PAIR_MAXB + 1];  // s_pre[b] = blocks of images < b
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (wave == 0) {
+// s_pre[b] = work items of images < b (wave 0 of a workgroup; items(n) per image)
+template <typename F>
+__device__ void nms_item_prefix(const NmsArgs& p, int nimg, int* s_pre, F items) {
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
     int run = 0;
     for (int b0 = 0; b0 < nimg; b0 += 64) {
       const int bb = b0 + lane;
       int cnt = 0;
       if (bb < nimg) {
         const int nn = min(p.ccount[bb], p.cap);
-        const int nbb = (nn + 63) >> 6;
-        cnt = nn <= NMS_FAST ? nbb * nbb
-              : (nn <= NMS_WIDE && p.wrows > 0 ? nbb * ((nn + NMS_WIDE_COLS - 1) / NMS_WIDE_COLS) : 0);
+        cnt = nn >= 1 && nn <= NMS_WIDE ? items(nn) : 0;
       }
       int incl = cnt;
 #pragma unroll
@@ -381,143 +382,100 @@ __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
     }
     if (lane == 0) s_pre[0] = 0;
   }
-  __syncthreads();
-  __shared__ uint64_t s_bits[4][64];
+}
+
+__device__ __forceinline__ int nms_item_image(const int* s_pre, int nimg, int g) {
+  int lo = 0, hi = nimg - 1;  // image b: s_pre[b] <= g < s_pre[b + 1]
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_pre[mid] <= g) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Rank items: 64 candidates (rows) against NMS_RANK_COLS columns, wave w taking 256 of them from LDS broadcasts;
+// persistent over all images' items, so a heavy image's items spread over the whole chip.
+__global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
+  __shared__ int s_pre[NMS_PAIR_MAXB + 1];
   __shared__ int s_cnt[4][64];
+  __shared__ uint64_t s_ck[4][256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  nms_item_prefix(p, nimg, s_pre, [](int nn) { return ((nn + 63) >> 6) * ((nn + NMS_RANK_COLS - 1) / NMS_RANK_COLS); });
+  __syncthreads();
   const int total = s_pre[nimg];
-  // a workgroup takes one 64 x 64 block at a time; wave w tests its rows against columns 16w .. 16w+15
   for (int g = blockIdx.x; g < total; g += gridDim.x) {
-    int lo = 0, hi = nimg - 1;  // image b: s_pre[b] <= g < s_pre[b + 1]
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_pre[mid] <= g) lo = mid;
-      else hi = mid - 1;
-    }
-    const int b = lo;
+    const int b = nms_item_image(s_pre, nimg, g);
     const int n = min(p.ccount[b], p.cap);
-    const int nb = (n + 63) >> 6;
     const int t = g - s_pre[b];
-    const float* cb = p.cbox + (int64_t)b * p.cap * 4;
     const float* sc = p.cscore + (int64_t)b * p.cap;
     const int* ix = p.cidx + (int64_t)b * p.cap;
-    const int* cc = p.ccls + (int64_t)b * p.cap;
-    if (n > NMS_FAST) {
-      // wide image: a rank item = 64 candidates (rows) against NMS_WIDE_COLS columns, wave w taking 256 of them;
-      // the item adds its count of smaller keys and one contribution into the row's 64-bit accumulator, and the
-      // row's last contribution (all ng column groups in) knows the final rank = the stable-sort position and
-      // writes order[rank] = slot
-      const int ng = (n + NMS_WIDE_COLS - 1) / NMS_WIDE_COLS;
-      const int bi = t / ng, gq = t - bi * ng;
-      const int i = bi * 64 + lane, ic = min(i, n - 1);
-      const uint64_t ki = make_key(sc[ic], ix[ic]);
-      const int c0 = gq * NMS_WIDE_COLS + wave * 256;
-      uint32_t kh[4], kl[4];
+    const int ng = (n + NMS_RANK_COLS - 1) / NMS_RANK_COLS;
+    const int bi = t / ng, gq = t - bi * ng;
+    const int i = bi * 64 + lane, ic = min(i, n - 1);
+    const int c0 = gq * NMS_RANK_COLS + wave * 256;
+    float csc[4];
+    int cix[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {  // the wave's 256 column keys, all loads issued first
-        const int jc = min(c0 + q * 64 + lane, n - 1);
-        const uint64_t k = make_key(sc[jc], ix[jc]);
-        kh[q] = (uint32_t)(k >> 32);
-        kl[q] = (uint32_t)k;
-      }
-      int below = 0;
+    for (int q = 0; q < 4; ++q) {  // this wave's 256 column keys (all loads issued first), then into LDS
+      const int jc = min(c0 + q * 64 + lane, n - 1);
+      csc[q] = sc[jc];
+      cix[q] = ix[jc];
+    }
+    const uint64_t ki = make_key(sc[ic], ix[ic]);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int ns = min(64, n - (c0 + q * 64));  // wave-uniform; <= 0 past the end
-        for (int s = 0; s < ns; ++s) {
-          const uint64_t k = ((uint64_t)__builtin_amdgcn_readlane(kh[q], s) << 32) | __builtin_amdgcn_readlane(kl[q], s);
-          below += k < ki;
-        }
-      }
-      s_cnt[wave][lane] = below;
-      __syncthreads();
-      if (wave == 0 && i < n) {
-        const int tot = s_cnt[0][lane] + s_cnt[1][lane] + s_cnt[2][lane] + s_cnt[3][lane];
-        const unsigned long long old =
-            atomicAdd(p.wacc + (int64_t)b * p.wrows + i, (1ull << 32) | (unsigned long long)(unsigned)tot);
-        if ((int)(old >> 32) == ng - 1) p.worder[(int64_t)b * p.wrows + (int)(uint32_t)old + tot] = i;
-      }
-      __syncthreads();
-      continue;
+    for (int q = 0; q < 4; ++q) s_ck[wave][q * 64 + lane] = make_key(csc[q], cix[q]);
+    __builtin_amdgcn_wave_barrier();
+    const int ns = max(0, min(256, n - c0));  // wave-uniform
+    int below = 0, s = 0;
+    for (; s + 4 <= ns; s += 4) {
+      const uint64_t k0 = s_ck[wave][s], k1 = s_ck[wave][s + 1], k2 = s_ck[wave][s + 2], k3 = s_ck[wave][s + 3];
+      below += (k0 < ki) + (k1 < ki) + (k2 < ki) + (k3 < ki);
     }
-    const int bi = t / nb, bj = t - bi * nb;
-    auto box_of = [&](int i) -> f32x4 {  // the sweep's class-offset box (nms_kernel load_box)
-      const f32x4 v = *reinterpret_cast<const f32x4*>(cb + (int64_t)i * 4);
-      const float c = float(cc[i]) * p.off_scale;
-      return f32x4{v[0] + c, v[1] + c, v[2] + c, v[3] + c};
-    };
-    const int i = bi * 64 + lane, j = bj * 64 + 16 * wave + (lane & 15);
-    const int ic = min(i, n - 1), jc = min(j, n - 1);
-    const f32x4 xi = box_of(ic), xj = box_of(jc);
-    const float ai = (xi[2] - xi[0]) * (xi[3] - xi[1]);
-    const uint64_t ki = make_key(sc[ic], ix[ic]), kj = make_key(sc[jc], ix[jc]);
-    const uint32_t kjh = (uint32_t)(kj >> 32), kjl = (uint32_t)kj;
-    const int ns = min(16, n - bj * 64 - 16 * wave);  // this wave's columns (may be <= 0)
-    uint64_t bits = 0;
-    int below = 0;
-    for (int s = 0; s < ns; ++s) {
-      const f32x4 y = f32x4{rlane(xj[0], s), rlane(xj[1], s), rlane(xj[2], s), rlane(xj[3], s)};
-      const uint64_t k = ((uint64_t)__builtin_amdgcn_readlane(kjh, s) << 32) | __builtin_amdgcn_readlane(kjl, s);
-      below += k < ki;
-      if (iou_gt(xi, ai, y, p.thr)) bits |= 1ull << (16 * wave + s);
-    }
-    s_bits[wave][lane] = bits;
+    for (; s < ns; ++s) below += s_ck[wave][s] < ki;
     s_cnt[wave][lane] = below;
     __syncthreads();
     if (wave == 0 && i < n) {
-      p.fmask[((int64_t)b * p.frows + i) * NMS_FW + bj] = s_bits[0][lane] | s_bits[1][lane] | s_bits[2][lane] | s_bits[3][lane];
-      p.frank[((int64_t)b * NMS_FW + bj) * p.frows + i] = s_cnt[0][lane] + s_cnt[1][lane] + s_cnt[2][lane] + s_cnt[3][lane];
+      const int tot = s_cnt[0][lane] + s_cnt[1][lane] + s_cnt[2][lane] + s_cnt[3][lane];
+      const int64_t o = (int64_t)b * p.wrows + i;
+      if (ng == 1) {
+        p.worder[(int64_t)b * p.wrows + tot] = i;  // the only contribution: no accumulator
+      } else {
+        const unsigned long long old = atomicAdd(p.wacc + o, (1ull << 32) | (unsigned long long)(unsigned)tot);
+        if ((int)(old >> 32) == ng - 1) p.worder[(int64_t)b * p.wrows + (int)(uint32_t)old + tot] = i;
+      }
     }
     __syncthreads();
   }
 }
 
-// Wide images, after nms_pair_kernel has ranked them: the IoU > thr bits of every pair of the first m = min(n,
-// max_nms) ranks, in rank space, row r word w bit s = IoU(rank r, rank 64w + s) > thr, for the 64 x 64 blocks on
-// and right of the diagonal (w >= r / 64; the sweep reads no other word).  Each wave takes one block at a time
-// (lane = row, the 64 columns broadcast by readlane), no barrier; persistent over all images' blocks.
-__global__ __launch_bounds__(256) void nms_wide_mask_kernel(NmsArgs p, int nimg) {
-  __shared__ int s_pre[NMS_PAIR_MAXB + 1];  // s_pre[b] = blocks of images < b
+// Rank-space IoU rows of the first m = min(n, max_nms) ranks, blocks on and right of the diagonal; each wave
+// takes one 64 x 64 block at a time (lane = row, the 64 columns as LDS broadcasts), no barrier.
+__global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs p, int nimg) {
+  __shared__ int s_pre[NMS_PAIR_MAXB + 1];
+  __shared__ f32x4 s_cb[4][64];
+  __shared__ float s_ca[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (wave == 0) {
-    int run = 0;
-    for (int b0 = 0; b0 < nimg; b0 += 64) {
-      const int bb = b0 + lane;
-      int cnt = 0;
-      if (bb < nimg) {
-        const int nn = min(p.ccount[bb], p.cap);
-        const int nbm = (min(nn, p.max_nms) + 63) >> 6;
-        cnt = nn > NMS_FAST && nn <= NMS_WIDE ? nbm * (nbm + 1) / 2 : 0;
-      }
-      int incl = cnt;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const int v = __shfl_up(incl, d);
-        if (lane >= d) incl += v;
-      }
-      if (bb < nimg) s_pre[bb + 1] = run + incl;
-      run += __shfl(incl, 63);
-    }
-    if (lane == 0) s_pre[0] = 0;
-  }
+  const int mx = p.max_nms;
+  nms_item_prefix(p, nimg, s_pre, [mx](int nn) {
+    const int nbm = (min(nn, mx) + 63) >> 6;
+    return nbm * (nbm + 1) / 2;
+  });
   __syncthreads();
   const int total = s_pre[nimg];
   for (int g = blockIdx.x * 4 + wave; g < total; g += gridDim.x * 4) {
-    int lo = 0, hi = nimg - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_pre[mid] <= g) lo = mid;
-      else hi = mid - 1;
-    }
-    const int b = lo;
+    const int b = nms_item_image(s_pre, nimg, g);
     const int n = min(p.ccount[b], p.cap);
     const int m = min(n, p.max_nms);
     const int nbm = (m + 63) >> 6;
-    int t = g - s_pre[b], bi = 0;  // upper-triangular block index -> (bi, bj >= bi)
-    while (t >= nbm - bi) {
-      t -= nbm - bi;
-      ++bi;
-    }
-    const int bj = bi + t;
+    // upper-triangular block index t -> (bi, bj >= bi): row bi starts at bi*nbm - bi*(bi-1)/2
+    const int t = g - s_pre[b];
+    const float tn = 2.f * nbm + 1.f;
+    int bi = (int)((tn - sqrtf(tn * tn - 8.f * (float)t)) * 0.5f);
+    bi = max(0, min(bi, nbm - 1));
+    while (bi > 0 && bi * nbm - bi * (bi - 1) / 2 > t) --bi;
+    while (bi + 1 < nbm && (bi + 1) * nbm - (bi + 1) * bi / 2 <= t) ++bi;
+    const int bj = bi + (t - (bi * nbm - bi * (bi - 1) / 2));
     const float* cb = p.cbox + (int64_t)b * p.cap * 4;
     const int* cc = p.ccls + (int64_t)b * p.cap;
     const int* ord = p.worder + (int64_t)b * p.wrows;
@@ -525,17 +483,19 @@ __global__ __launch_bounds__(256) void nms_wide_mask_kernel(NmsArgs p, int nimg)
     const int si = ord[min(r, m - 1)], sj = ord[min(bj * 64 + lane, m - 1)];
     const f32x4 vi = *reinterpret_cast<const f32x4*>(cb + (int64_t)si * 4);
     const f32x4 vj = *reinterpret_cast<const f32x4*>(cb + (int64_t)sj * 4);
-    const float ci = float(cc[si]) * p.off_scale, cj = float(cc[sj]) * p.off_scale;
+    const float ci = float(cc[si]) * p.off_scale, cj = float(cc[sj]) * p.off_scale;  // boxes + cls * max_wh
     const f32x4 xi = f32x4{vi[0] + ci, vi[1] + ci, vi[2] + ci, vi[3] + ci};
     const f32x4 xj = f32x4{vj[0] + cj, vj[1] + cj, vj[2] + cj, vj[3] + cj};
     const float ai = (xi[2] - xi[0]) * (xi[3] - xi[1]);
+    s_cb[wave][lane] = xj;
+    s_ca[wave][lane] = (xj[2] - xj[0]) * (xj[3] - xj[1]);
+    __builtin_amdgcn_wave_barrier();
     const int ns = min(64, m - bj * 64);
     uint64_t bits = 0;
-    for (int s = 0; s < ns; ++s) {
-      const f32x4 y = f32x4{rlane(xj[0], s), rlane(xj[1], s), rlane(xj[2], s), rlane(xj[3], s)};
-      if (iou_gt(xi, ai, y, p.thr)) bits |= 1ull << s;
-    }
-    if (r < m) p.wmask[((int64_t)b * p.wrows + r) * p.wwords + bj] = bits;
+    for (int s = 0; s < ns; ++s)
+      if (iou_gt(xi, ai, s_cb[wave][s], s_ca[wave][s], p.th)) bits |= 1ull << s;
+    __builtin_amdgcn_wave_barrier();  // every lane's reads are done before the next block overwrites the columns
+    if (r < m) p.wmask[(int64_t)b * p.wrows * p.wwords + (int64_t)r * nbm + bj] = bits;  // rows of nbm words
   }
 }
 
@@ -549,7 +509,7 @@ __global__ __launch_bounds__(256) void nms_wide_mask_kernel(NmsArgs p, int nimg)
 template <bool GROUPS>
 __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   // LDS: sort keys (64 KB) are reused for the first 4096 sorted boxes after sorting.
-  // sort keys | sort slots | suppression flags, one buffer: the pair-matrix path stages its mask rows
+  // sort keys | sort slots | suppression flags, one buffer: the pair-matrix path stages a chunk's rows
   // (NMS_FAST x NMS_FW words = 128 KiB) over all three
   __shared__ __align__(16) unsigned char s_raw[NMS_SORT_LDS * 12 + NMS_MAX_FLAGS];
   static_assert(NMS_FAST * NMS_FW * 8 <= NMS_SORT_LDS * 12 + NMS_MAX_FLAGS, "pair-matrix rows fit the sort buffers");
@@ -557,8 +517,6 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   int* s_vals = reinterpret_cast<int*>(s_raw + NMS_SORT_LDS * 8);
   unsigned char* removed = s_raw + NMS_SORT_LDS * 12;
   __shared__ int kept_slot[NMS_MAX_DET];
-  __shared__ int s_order[NMS_FAST];
-  __shared__ uint64_t s_dw[NMS_FAST];
   __shared__ int s_wsum[NMS_THREADS / 64];
   __shared__ f32x4 chunk_box[64];
   __shared__ float chunk_area[64];
@@ -568,133 +526,14 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   constexpr int LDS_BOXES = NMS_SORT_LDS * 8 / 16;
 
   NMS_STAMP(0, __builtin_amdgcn_s_memrealtime());
-  bool kept_rank = false;  // the wide path keeps ranks in kept_slot (slot = worder[rank])
+  bool kept_rank = false;  // the pair-matrix path keeps ranks in kept_slot (slot = worder[rank])
   const int b = GROUPS ? blockIdx.x / NMS_GROUPS : blockIdx.x;
   const int grp = GROUPS ? blockIdx.x % NMS_GROUPS : 0;
   int n = min(p.ccount[b], p.cap);
   const float* sc = p.cscore + (int64_t)b * p.cap;
   const int* ix = p.cidx + (int64_t)b * p.cap;
-  if (p.fast && n <= NMS_FAST) {
-    // ---- pair-matrix path (nms_pair_kernel filled fmask / frank for this image)
-    if constexpr (GROUPS) {
-      if (grp != 0) {  // the whole image is group 0's
-        if (threadIdx.x == 0) p.gcount[(int64_t)b * NMS_GROUPS + grp] = 0;
-        return;
-      }
-    }
-    const int m = min(n, p.max_nms);  // the reference's argsort(descending)[:max_nms]
-    const int nb = (n + 63) >> 6;
-    const int* rpart = p.frank + (int64_t)b * NMS_FW * p.frows;
-    // every global load of this thread is issued before the first one is used (fixed trip counts)
-    static_assert(NMS_FAST == NMS_THREADS, "one candidate per thread");
-    {
-      const int i = threadIdx.x;
-      int part[NMS_FW];
-#pragma unroll
-      for (int w = 0; w < NMS_FW; ++w) part[w] = i < n && w < nb ? rpart[w * p.frows + i] : 0;
-      int r = 0;
-#pragma unroll
-      for (int w = 0; w < NMS_FW; ++w) r += part[w];
-      if (i < n && r < m) s_order[r] = i;
-    }
-    uint64_t* smask = reinterpret_cast<uint64_t*>(s_raw);  // [n][NMS_FW]
-    {
-      const uint64_t* gm = p.fmask + (int64_t)b * p.frows * NMS_FW;
-      uint64_t v[NMS_FW];
-#pragma unroll
-      for (int k = 0; k < NMS_FW; ++k) {
-        const int e = threadIdx.x + k * NMS_THREADS;
-        v[k] = e < n * NMS_FW && (e & (NMS_FW - 1)) < nb ? gm[e] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < NMS_FW; ++k) {
-        const int e = threadIdx.x + k * NMS_THREADS;
-        if (e < n * NMS_FW) smask[mslot(e >> 4, e & (NMS_FW - 1))] = v[k];
-      }
-    }
-    __syncthreads();
-    NMS_STAMP(1, __builtin_amdgcn_s_memrealtime());
-    NMS_STAMP(2, __builtin_amdgcn_s_memrealtime());
-    NMS_STAMP(6, (unsigned long long)m);
-    // within-block suppression words in rank space: s_dw[r] bit s = row of rank r suppresses rank
-    // 64*(r/64) + s, for s > r%64 (wave w builds block w: the column candidates are wave-uniform)
-    // (branch-free body: the 64 row reads of a lane are issued back to back)
-    if ((int)(threadIdx.x & ~63) < m) {
-      const int r = threadIdx.x, k0 = r & ~63, rl = r & 63;
-      const int cr = r < m ? s_order[r] : 0;  // lane rl holds the candidate of rank k0 + rl (this wave's block)
-      const int send = min(64, m - k0);
-      uint64_t dw = 0;
-#pragma unroll 8
-      for (int q = 0; q < 64; ++q) {
-        const int cq = __builtin_amdgcn_readlane(cr, q);
-        const uint64_t bit = (smask[mslot(cr, (cq >> 6) & (NMS_FW - 1))] >> (cq & 63)) & 1ull;
-        dw |= (q > rl && q < send) ? bit << q : 0ull;
-      }
-      if (r < m) s_dw[r] = dw;
-    }
-    __syncthreads();
-    NMS_STAMP(4, __builtin_amdgcn_s_memrealtime());
-    if (threadIdx.x < 64) {  // one wave sweeps the rank blocks in order
-      const int lane = threadIdx.x;
-      uint64_t rem = 0;  // lane w < nb: removed flags of candidates 64w .. 64w+63
-      int nk = 0;
-      for (int t0 = 0; t0 < m && nk < p.max_det; t0 += 64) {
-        const bool valid = t0 + lane < m;
-        const int myc = valid ? s_order[t0 + lane] : 0;
-        const uint64_t dw = valid ? s_dw[t0 + lane] : 0ull;
-        // alive = not removed by a kept candidate of an earlier block
-        const int wsrc = myc >> 6;
-        const uint32_t rlo = __shfl((uint32_t)rem, wsrc), rhi = __shfl((uint32_t)(rem >> 32), wsrc);
-        const uint64_t rw = ((uint64_t)rhi << 32) | rlo;
-        const uint64_t M = __ballot(valid && !((rw >> (myc & 63)) & 1));
-        const int nk0 = nk;
-        // greedy inside the block: K_r = M_r & !(any s < r in K with D[s] bit r).  Iterated from K = M as
-        // K' = M & ~OR_{s in K} D[s] (one wave-wide OR per step) it reaches that unique fixed point: after t
-        // steps the first t ranks are final, and steps stop as soon as K repeats -- a few for NMS clusters,
-        // where the scalar walk paid one dependent step per kept rank
-        uint64_t K = M;
-        for (;;) {
-          const uint64_t W = __ockl_wfred_or_u64((K >> lane) & 1 ? dw : 0ull);
-          const uint64_t Kn = M & ~W;
-          if (Kn == K) break;
-          K = Kn;
-        }
-        // keep[:max_det]: the greedy stops at max_det keeps, i.e. the lowest ranks of K
-        for (int extra = __popcll(K) - (p.max_det - nk0); extra > 0; --extra) K &= ~(1ull << (63 - __clzll(K)));
-        nk = nk0 + __popcll(K);
-        if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = myc;
-        // the kept candidates' rows join the removed flags (8 row reads in flight at a time)
-        // (branch-free: all 8 reads are issued before the first OR)
-        while (K) {
-          int c[8];
-          bool ok[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) {
-            const int t = __ffsll((long long)K) - 1;  // -1 once K is empty
-            K &= K - 1;
-            ok[q] = t >= 0;
-            c[q] = __builtin_amdgcn_readlane(myc, t & 63);
-          }
-          uint64_t row[8];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) row[q] = smask[mslot(c[q], lane & (NMS_FW - 1))];
-#pragma unroll
-          for (int q = 0; q < 8; ++q) rem |= ok[q] && lane < nb ? row[q] : 0ull;
-        }
-      }
-      if (lane == 0) s_nk = nk;
-    }
-    __syncthreads();
-    NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
-    NMS_STAMP(5, 0ull);
-  } else if (p.fast && p.wrows > 0 && n <= NMS_WIDE) {
-    // ---- wide pair-matrix path: the ranks and rank-space IoU rows come from nms_pair_kernel and
-    // nms_wide_mask_kernel; the sweep walks the ranks in chunks of NMS_FAST.  Per chunk: the ranks not yet
-    // removed by an earlier chunk's kept rows are compacted (rank order kept), their rows' words over the chunk
-    // are staged in LDS and the chunk runs exactly the pair-matrix sweep above (within-block words, fixed-point
-    // block greedy, kept rows ORed into the chunk's removed flags); then the rows of the chunk's new keeps are
-    // ORed, over the ranks right of the chunk, into the image's removed bits -- so a chunk only ever sweeps
-    // ranks nothing kept before it suppresses.
+  if (p.fast && p.wrows > 0 && n <= NMS_WIDE) {
+    // ---- pair-matrix path (nms_pair_kernel ranked the image, nms_mask_kernel wrote its rank-space rows)
     if constexpr (GROUPS) {
       if (grp != 0) {  // the whole image is group 0's
         if (threadIdx.x == 0) p.gcount[(int64_t)b * NMS_GROUPS + grp] = 0;
@@ -702,86 +541,75 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       }
     }
     kept_rank = true;
-    const int m = min(n, p.max_nms);
+    const int m = min(n, p.max_nms);  // the reference's argsort(descending)[:max_nms]
     const int W = (m + 63) >> 6;
     uint64_t* wrem = reinterpret_cast<uint64_t*>(chunk_box);  // removed bits of ranks 0 .. NMS_WIDE - 1
-    static_assert(sizeof(chunk_box) >= NMS_WIDE / 8, "wide removed bits alias chunk_box");
-    for (int w = threadIdx.x; w < NMS_WIDE / 64; w += NMS_THREADS) wrem[w] = 0ull;
-    unsigned long long* acc = p.wacc + (int64_t)b * p.wrows;
-    for (int i = threadIdx.x; i < n; i += NMS_THREADS) acc[i] = 0ull;  // ready for the next call (pair kernel done)
+    static_assert(sizeof(chunk_box) >= NMS_WIDE / 8, "removed bits alias chunk_box");
+    const int t = threadIdx.x, lane = t & 63;
+    for (int w = t; w < W; w += NMS_THREADS) wrem[w] = 0ull;
+    if (n > NMS_RANK_COLS) {  // the rank accumulators nms_pair_kernel used, zero again for the next call
+      unsigned long long* acc = p.wacc + (int64_t)b * p.wrows;
+      for (int i = t; i < n; i += NMS_THREADS) acc[i] = 0ull;
+    }
     const uint64_t* gm = p.wmask + (int64_t)b * p.wrows * p.wwords;
-    uint64_t* smask = reinterpret_cast<uint64_t*>(s_raw);  // [compact position][NMS_FW], mslot order
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint64_t* smask = reinterpret_cast<uint64_t*>(s_raw);  // [local rank][NMS_FW], mslot order
     if (t == 0) s_nk = 0;
     __syncthreads();
+    NMS_STAMP(1, __builtin_amdgcn_s_memrealtime());
+#ifdef YDBL_NMS_STAMPS
+    unsigned long long t_last = __builtin_amdgcn_s_memrealtime(), ta = 0, tb = 0, tc = 0;
+    int rounds = 0;
+#endif
     for (int R0 = 0; R0 < m; R0 += NMS_FAST) {
+#ifdef YDBL_NMS_STAMPS
+      ++rounds;
+#endif
       const int nk_prev = s_nk;
       if (nk_prev >= p.max_det) break;
-      const int L = min(NMS_FAST, m - R0);
-      // (a) compaction of the chunk's live ranks: s_order[pos] = local rank (0 .. L-1)
-      const int r = R0 + t;
-      const bool alive = t < L && !((wrem[r >> 6] >> (r & 63)) & 1ull);
-      const uint64_t bal = __ballot(alive);
-      if (lane == 0) s_wsum[wave] = __popcll(bal);
-      __syncthreads();
-      int off = 0, cnt = 0;
-#pragma unroll
-      for (int w = 0; w < NMS_THREADS / 64; ++w) {
-        const int v = s_wsum[w];
-        off += w < wave ? v : 0;
-        cnt += v;
-      }
-      if (alive) s_order[off + __popcll(bal & ((1ull << lane) - 1))] = t;
-      __syncthreads();
-      if (cnt == 0) continue;
-      // (b) rows of the live ranks, words of this chunk (words left of a row's own block were not written: 0)
-      const int w0 = R0 >> 6, nbw = (L + 63) >> 6;
+      const int L = min(NMS_FAST, m - R0), nbw = (L + 63) >> 6, w0 = R0 >> 6;
+      // (a) the chunk's rows, words of this chunk; rows of ranks an earlier chunk removed stay 0 (never read),
+      // and so do the words left of a row's own block (never written)
       {
         uint64_t v[NMS_FW];
 #pragma unroll
         for (int k = 0; k < NMS_FW; ++k) {
-          const int e = t + k * NMS_THREADS, pos = e >> 4, w = e & (NMS_FW - 1);
-          v[k] = 0ull;
-          if (pos < cnt && w < nbw) {
-            const int rr = R0 + s_order[pos];
-            if (w0 + w >= (rr >> 6)) v[k] = gm[(int64_t)rr * p.wwords + w0 + w];
-          }
+          const int e = t + k * NMS_THREADS, pos = e >> 4, w = e & (NMS_FW - 1), r = R0 + pos;
+          const bool ok = pos < L && w < nbw && w >= (pos >> 6) && !((wrem[min(r, m - 1) >> 6] >> (r & 63)) & 1ull);
+          v[k] = ok ? gm[(int64_t)r * W + w0 + w] : 0ull;
         }
 #pragma unroll
         for (int k = 0; k < NMS_FW; ++k) {
           const int e = t + k * NMS_THREADS;
-          if ((e >> 4) < cnt) smask[mslot(e >> 4, e & (NMS_FW - 1))] = v[k];
+          if ((e >> 4) < L) smask[mslot(e >> 4, e & (NMS_FW - 1))] = v[k];
         }
       }
       __syncthreads();
-      // (c) within-block words over compact positions (columns: local ranks)
-      if ((t & ~63) < cnt) {
-        const int k0 = t & ~63, rl = t & 63;
-        const int cr = t < cnt ? s_order[t] : 0;
-        const int send = min(64, cnt - k0);
-        uint64_t dw = 0;
-#pragma unroll 8
-        for (int q = 0; q < 64; ++q) {
-          const int cq = __builtin_amdgcn_readlane(cr, q);
-          const uint64_t bit = (smask[mslot(t, (cq >> 6) & (NMS_FW - 1))] >> (cq & 63)) & 1ull;
-          dw |= (q > rl && q < send) ? bit << q : 0ull;
-        }
-        if (t < cnt) s_dw[t] = dw;
-      }
-      __syncthreads();
-      // (d) the sweep of the pair-matrix path over the compact positions
+      NMS_TICK(ta);
+      // (b) one wave sweeps the chunk's 64-rank blocks in order
       if (t < 64) {
-        uint64_t rem = 0;  // lane w < nbw: removed flags of local ranks 64w .. 64w+63
+        uint64_t rem = lane < nbw ? wrem[w0 + lane] : ~0ull;  // lane w: removed flags of local ranks 64w .. 64w+63
         int nk = nk_prev;
-        for (int t0 = 0; t0 < cnt && nk < p.max_det; t0 += 64) {
-          const bool valid = t0 + lane < cnt;
-          const int myc = valid ? s_order[t0 + lane] : 0;
-          const uint64_t dw = valid ? s_dw[t0 + lane] : 0ull;
-          const int wsrc = myc >> 6;
-          const uint32_t rlo = __shfl((uint32_t)rem, wsrc), rhi = __shfl((uint32_t)(rem >> 32), wsrc);
-          const uint64_t rw = ((uint64_t)rhi << 32) | rlo;
-          const uint64_t M = __ballot(valid && !((rw >> (myc & 63)) & 1));
+        auto diag = [&](int blk) -> uint64_t {  // the lane's row, its own block's word
+          const int c = blk * 64 + lane;
+          return c < L ? smask[mslot(c, blk)] : 0ull;
+        };
+        uint64_t nx = diag(0);  // read one block ahead
+        for (int blk = 0; blk < nbw && nk < p.max_det; ++blk) {
+          const uint64_t drow = nx;
+          if (blk + 1 < nbw) nx = diag(blk + 1);
+          const int cnt = min(64, L - blk * 64);
+          const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1);
+          // (a bpermute, not v_readlane: a readlane of the 64-bit word with the loop's block index read the high
+          // half from another lane in this kernel -- the keep sets came out wrong)
+          const uint64_t rw = ((uint64_t)__shfl((uint32_t)(rem >> 32), blk) << 32) | __shfl((uint32_t)rem, blk);
+          const uint64_t M = valid & ~rw;  // live = not removed by a kept candidate of an earlier block
+          if (!M) continue;
+          const uint64_t dw = lane < 63 ? drow & (~0ull << (lane + 1)) : 0ull;  // later ranks of the block it suppresses
           const int nk0 = nk;
+          // greedy inside the block: K_r = M_r & !(any s < r in K with D[s] bit r).  Iterated from K = M as
+          // K' = M & ~OR_{s in K} D[s] (one wave-wide OR per step) it reaches that unique fixed point: after t
+          // steps the first t ranks are final, and steps stop as soon as K repeats -- a few for NMS clusters,
+          // where a scalar walk would pay one dependent step per kept rank
           uint64_t K = M;
           for (;;) {
             const uint64_t Wo = __ockl_wfred_or_u64((K >> lane) & 1 ? dw : 0ull);
@@ -789,30 +617,47 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
             if (Kn == K) break;
             K = Kn;
           }
+#ifdef YDBL_NMS_DUMP
+          if (blockIdx.x == 1 && R0 == 0 && blk == 4) {
+            g_nms_stamps[2000 + lane] = drow;
+            g_nms_stamps[2100 + lane] = dw;
+            if (lane == 0) { g_nms_stamps[2200] = M; g_nms_stamps[2201] = K; g_nms_stamps[2202] = rw; g_nms_stamps[2203] = nk0; }
+          }
+#endif
+          // keep[:max_det]: the greedy stops at max_det keeps, i.e. the lowest ranks of K
           for (int extra = __popcll(K) - (p.max_det - nk0); extra > 0; --extra) K &= ~(1ull << (63 - __clzll(K)));
           nk = nk0 + __popcll(K);
-          if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = R0 + myc;  // a rank here
+          if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = R0 + blk * 64 + lane;  // a rank
+          // the kept candidates' rows join the removed flags (16 row reads in flight at a time; branch-free: all
+          // 16 reads are issued before the first OR)
           while (K) {
-            int c[8];
-            bool ok[8];
+            int c[16];
+            bool ok[16];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-              const int tt = __ffsll((long long)K) - 1;
+            for (int q = 0; q < 16; ++q) {
+              const int tt = __ffsll((long long)K) - 1;  // -1 once K is empty
               K &= K - 1;
               ok[q] = tt >= 0;
-              c[q] = t0 + (tt & 63);  // the kept candidate's compact position = its staged row
+              c[q] = blk * 64 + (tt & 63);
             }
-            uint64_t row[8];
+            uint64_t row[16];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) row[q] = smask[mslot(c[q], lane & (NMS_FW - 1))];
+            for (int q = 0; q < 16; ++q) row[q] = smask[mslot(c[q], lane & (NMS_FW - 1))];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) rem |= ok[q] && lane < nbw ? row[q] : 0ull;
+            for (int q = 0; q < 16; ++q) rem |= ok[q] && lane < nbw ? row[q] : 0ull;
           }
+#ifdef YDBL_NMS_DUMP
+          if (blockIdx.x == 1 && R0 == 0 && blk < 5) {
+            if (lane < 16) g_nms_stamps[3000 + blk * 16 + lane] = rem;
+            if (lane == 0) { g_nms_stamps[3100 + blk] = M; g_nms_stamps[3110 + blk] = rw; }
+          }
+#endif
         }
         if (lane == 0) s_nk = nk;
       }
       __syncthreads();
-      // (e) the new keeps' rows, right of the chunk, into the image's removed bits (8 loads in flight per thread)
+      NMS_TICK(tb);
+      // (c) the new keeps' rows, right of the chunk, into the image's removed bits (8 loads in flight per thread)
       const int nk_now = s_nk, wbeg = w0 + NMS_FW;
       if (nk_now < p.max_det && wbeg < W && nk_now > nk_prev) {
         const int span = W - wbeg, tot = (nk_now - nk_prev) * span;
@@ -824,7 +669,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
             const int e = e0 + q * NMS_THREADS;
             const int k = e / span, w = wbeg + (e - k * span);
             wd[q] = e < tot ? w : -1;
-            v[q] = e < tot ? gm[(int64_t)kept_slot[nk_prev + k] * p.wwords + w] : 0ull;
+            v[q] = e < tot ? gm[(int64_t)kept_slot[nk_prev + k] * W + w] : 0ull;
           }
 #pragma unroll
           for (int q = 0; q < 8; ++q)
@@ -832,8 +677,15 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
         }
       }
       __syncthreads();
+      NMS_TICK(tc);
     }
+    NMS_STAMP(2, __builtin_amdgcn_s_memrealtime());
     NMS_STAMP(3, __builtin_amdgcn_s_memrealtime());
+    NMS_STAMP(6, (unsigned long long)m);
+#ifdef YDBL_NMS_STAMPS
+    NMS_STAMP(5, (unsigned long long)rounds);
+    NMS_STAMP(7, ta); NMS_STAMP(8, tb); NMS_STAMP(9, tc);
+#endif
   } else {
     bool listed = false;  // GROUPS: this group's (key, slot) list is already in s_keys / s_vals
     if constexpr (GROUPS) {
@@ -965,7 +817,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int j = c0 + 4 * wave + q;
-            if (j > i && j < m_cur && !removed[j] && iou_gt(bi, ai, box_at(j), p.thr)) bits |= 1u << q;
+            if (j > i && j < m_cur && !removed[j] && iou_gt(bi, ai, box_at(j), p.th)) bits |= 1u << q;
           }
         }
         cmask[lane][wave] = (unsigned char)bits;
@@ -1034,7 +886,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
               }
 #pragma unroll
               for (int u = 0; u < 8; ++u)
-                if (q0 + u * G < ck) sup |= iou_gt(bq[u], aq[u], bj, p.thr);
+                if (q0 + u * G < ck) sup |= iou_gt(bq[u], aq[u], bj, p.th);
             }
             if (sup) removed[j] = 1;
           }
@@ -1283,13 +1135,11 @@ extern "C" int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream) 
 }
 
 // [global sort keys n*L x 8 B][sort slots n*L x 4 B][group keys n*G*gk x 8 B][group slots x 4 B][counts n*G x 4 B]
-// [pad to 8 B][pair-matrix rows n*R*NMS_FW x 8 B][partial ranks n*NMS_FW*R x 4 B]
+// [pad to 8 B][rank accumulators n*R x 8 B][rank-space rows n*R x R/64 x 8 B][order n*R x 4 B]
 static int64_t nms_sort_len(int32_t cap) { return cap <= NMS_SORT_LDS ? 0 : next_pow2(cap); }
 static int32_t nms_group_len(int32_t cap) { return cap < NMS_MAX_DET ? cap : NMS_MAX_DET; }
-// rows per image of the pair-matrix workspace: candidates up to NMS_FAST, in whole 64-row blocks
-static int32_t nms_fast_rows(int32_t cap) { return (std::min(cap, NMS_FAST) + 63) / 64 * 64; }
-// rows per image of the wide path (0: cap <= NMS_FAST, no image can be wide)
-static int32_t nms_wide_rows(int32_t cap) { return cap <= NMS_FAST ? 0 : (std::min(cap, NMS_WIDE) + 63) / 64 * 64; }
+// rows per image of the pair-matrix path: candidates up to NMS_WIDE, in whole 64-row blocks
+static int32_t nms_rank_rows(int32_t cap) { return (std::min(cap, NMS_WIDE) + 63) / 64 * 64; }
 
 #ifdef YDBL_NMS_STAMPS
 extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
@@ -1300,11 +1150,9 @@ extern "C" int ydbl_nms_debug_stamps(unsigned long long* out, int32_t n) {
 extern "C" int64_t ydbl_nms_workspace(int32_t n, int32_t cap, int32_t max_nms) {
   (void)max_nms;
   if (n < 1 || cap < 1) return 16;
-  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap), R = nms_fast_rows(cap), RW = nms_wide_rows(cap);
-  // + pair-matrix rows (u64 x NMS_FW) and partial ranks (int x NMS_FW) per candidate row, 8-byte aligned
-  // + wide rows: rank accumulator (u64), order (int), IoU row (RW / 64 u64) per row
-  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 8 + (int64_t)n * R * NMS_FW * 12 + 16 +
-         (int64_t)n * RW * (12 + RW / 8) + 16;
+  const int64_t L = nms_sort_len(cap), gk = nms_group_len(cap), R = nms_rank_rows(cap);
+  // + per pair-matrix row: rank accumulator (u64), order entry (int), rank-space IoU row (R / 64 u64)
+  return (int64_t)n * L * 12 + (int64_t)n * NMS_GROUPS * (gk * 12 + 4) + 8 + (int64_t)n * R * (12 + R / 8) + 16;
 }
 
 extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
@@ -1331,28 +1179,29 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   a.gcount = a.gslot + (int64_t)d->n * NMS_GROUPS * a.gk;
   a.cap = d->cap;
   a.thr = d->iou_thres; a.max_det = d->max_det; a.max_nms = d->max_nms;
+  {  // the fp32 thresholds of iou_gt: a = the largest float <= thr
+    float f = (float)d->iou_thres;
+    if ((double)f > d->iou_thres) f = std::nextafter(f, -1.f);
+    a.th.a = f;
+    a.th.hi = f * (1.f + 2e-5f) + 1e-30f;
+    a.th.lo = f * (1.f - 2e-5f) - 1e-30f;
+  }
   a.off_scale = d->agnostic ? 0.f : d->max_wh;
   a.clip_w = d->clip_w; a.clip_h = d->clip_h;
   a.out = d->out; a.out_count = d->out_count;
   a.ostride = d->out_stride ? d->out_stride : (int64_t)d->max_det * 6;
   a.cstride = d->count_stride ? d->count_stride : 1;
-  a.frows = nms_fast_rows(d->cap);
-  a.fmask = reinterpret_cast<uint64_t*>(a.gcount + (int64_t)d->n * NMS_GROUPS + ((int64_t)d->n * NMS_GROUPS & 1));
-  a.frank = reinterpret_cast<int*>(a.fmask + (int64_t)d->n * a.frows * NMS_FW);
-  a.wrows = nms_wide_rows(d->cap);
+  a.wrows = nms_rank_rows(d->cap);
   a.wwords = a.wrows / 64;
-  {
-    const int64_t fr = (int64_t)d->n * NMS_FW * a.frows;  // ints of frank, then 8-byte alignment
-    a.wacc = reinterpret_cast<unsigned long long*>(a.frank + fr + (fr & 1));
-    a.wmask = reinterpret_cast<uint64_t*>(a.wacc + (int64_t)d->n * a.wrows);
-    a.worder = reinterpret_cast<int*>(a.wmask + (int64_t)d->n * a.wrows * a.wwords);
-  }
-  const char* we = getenv("YDBL_NMS_WIDE");  // A/B switch (read per launch: tests): 0 = no wide pair-matrix path
-  if (we && *we == '0') a.wrows = 0;
+  a.wacc = reinterpret_cast<unsigned long long*>(a.gcount + (int64_t)d->n * NMS_GROUPS + ((int64_t)d->n * NMS_GROUPS & 1));
+  a.wmask = reinterpret_cast<uint64_t*>(a.wacc + (int64_t)d->n * a.wrows);
+  a.worder = reinterpret_cast<int*>(a.wmask + (int64_t)d->n * a.wrows * a.wwords);
   const char* fe = getenv("YDBL_NMS_FAST");  // A/B switch (read per launch: tests): 0 = sort + chunked sweep only
   a.fast = !(fe && *fe == '0') && d->n <= NMS_PAIR_MAXB;
-  if (a.fast) nms_pair_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
-  if (a.fast && a.wrows > 0) nms_wide_mask_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
+  if (a.fast) {
+    nms_pair_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
+    nms_mask_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
+  }
   // class-split sweep + merge (non-agnostic); the one-workgroup-per-image form for agnostic NMS or on request
   const char* ev = getenv("YDBL_NMS_GROUPS");  // A/B switch (read per launch: tests): 0 = one workgroup per image
   if (d->agnostic || d->per_image || (ev && *ev == '0')) {

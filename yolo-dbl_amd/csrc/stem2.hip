@@ -21,6 +21,8 @@
 // HBM traffic is the input once (+ halo re-reads, mostly L2 hits) and the output once.
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "conv_common.hpp"
 
 namespace ydbl {
@@ -144,7 +146,16 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   constexpr int IT = (TASKS + 255) / 256;
   f32x4 v[IT][3];
   bool okv[IT];  // the task's pixels lie inside the image (record slot 3 = 1: the folded bias)
-  auto load_window = [&](const Tile& tl) {  // the batch, read once: nontemporal loads (batchmax.hip)
+  // A bound input (predict() reading the caller's batch in place, include/ydbl.h ydbl_input_bind) arrives cold and is
+  // read once: nontemporal loads, which skip the Infinity-Cache allocation that would evict dirty activation lines
+  // (batchmax.hip).  The session's own staging buffer (no binding: the bench path) is read with plain loads: in the
+  // graph it was just written by the copy in, and nontemporal loads cost it 3-4 us per bs16 launch
+  // (profiles/r06/r06_stem2_nt_ab.txt).
+  auto ld = [](const auto* ptr, auto nt) {
+    if constexpr (decltype(nt)::value) return __builtin_nontemporal_load(ptr);
+    else return *ptr;
+  };
+  auto load_window = [&](const Tile& tl, auto nt) {
     const float* xb = x + (int64_t)tl.img * 3 * plane;
     if constexpr (V4) {
       const int A = tl.X0 - 3;
@@ -158,7 +169,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
         const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
         for (int c = 0; c < 3; ++c)
-          v[u][c] = ok ? __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(xb + c * plane + o))
+          v[u][c] = ok ? ld(reinterpret_cast<const f32x4*>(xb + c * plane + o), nt)
                        : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     } else {
@@ -171,7 +182,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
         okv[u] = ok;
         const int64_t o = ok ? (int64_t)iy * W + ix : 0;
 #pragma unroll
-        for (int ch = 0; ch < 3; ++ch) v[u][ch][0] = ok ? __builtin_nontemporal_load(xb + ch * plane + o) : 0.f;
+        for (int ch = 0; ch < 3; ++ch) v[u][ch][0] = ok ? ld(xb + ch * plane + o, nt) : 0.f;
       }
     }
   };
@@ -250,7 +261,8 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   }
 #endif
   const Tile tl = tile_of(blockIdx.x);
-  load_window(tl);
+  if (ib.x) load_window(tl, std::true_type{});
+  else load_window(tl, std::false_type{});
   {
     store_window();
     __syncthreads();

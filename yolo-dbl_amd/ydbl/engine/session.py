@@ -250,8 +250,8 @@ class DetectSession:
     def _set_slot(self, k: int, det: torch.Tensor | None = None, count: torch.Tensor | None = None):
         """Point the plans' input-reading launches at binding slot k and their NMS outputs at det / count (default:
         the session's own), before a capture; the C-ABI copies both into the kernel arguments at launch."""
-        for i, cm in enumerate(self._owners()):
-            cm.set_bind(self.bind_ptrs[k, i:i + 1], self.bind_amax[k])
+        for i, cm in enumerate(self._owners()):  # slot 0: no binding, the plans read their own staging buffers
+            cm.set_bind(self.bind_ptrs[k, i:i + 1] if k else None, self.bind_amax[k])
         det = self.det if det is None else det
         count = self.count if count is None else count
         for nd, (a, b) in zip(self._nms_descs(), self.bounds if self.children else [(0, self.batch)]):

@@ -338,6 +338,7 @@ class DetectionModel(nn.Module):
         cm.bind_holders = [st.args[0].bind if st.fn.__name__ == "ydbl_conv_stem2" else st.args[-1]
                            for st in plan.steps if st.fn.__name__ in ("ydbl_conv_stem2", "ydbl_conv_stem",
                                                                        "ydbl_input_nchw_to_nhwc")]
+        cm.set_bind(None)  # the plan's own staging buffer, read directly (DetectSession slot 0)
         return cm
 
 
@@ -352,11 +353,13 @@ class CompiledModel:
         """Reference-layout per-level outputs x[i] = cat(box, cls) as NCHW views (no copy)."""
         return [lv.nchw() for lv in self.levels]
 
-    def set_bind(self, ptr: torch.Tensor, amax: torch.Tensor):
+    def set_bind(self, ptr: torch.Tensor | None, amax: torch.Tensor | None = None):
         """Point every input-reading launch at another binding (device int64 batch-pointer word, fp32 maximum); the
-        C-ABI copies the record into the kernel arguments at launch, so a graph captured afterwards keeps it."""
+        C-ABI copies the record into the kernel arguments at launch, so a graph captured afterwards keeps it.
+        None: no binding -- the launches read the plan's own staging buffer and scale from their arguments, with no
+        dependent pointer / maximum load ahead of the input window (the session's own launches, the bench path)."""
         for h in self.bind_holders:
-            h.x, h.amax = ptr.data_ptr(), amax.data_ptr()
+            h.x, h.amax = (None, None) if ptr is None else (ptr.data_ptr(), amax.data_ptr())
 
 
 def _propagate_shapes(layers, batch, h, w, ch):
