@@ -99,8 +99,15 @@ typedef struct {
    * dequantizes the fp32 accumulator before bias and activation. */
   const float* dq;
   float qscale;
+  /* optional split-K scratch (fp32 partial tiles): workspace_bytes >= ydbl_conv_workspace(d) lets the deep-K
+   * wave-split-K path split its k-loop over up to 4 workgroups per tile when the map gives too few tiles to fill the
+   * chip (the 20^2 / 40^2 maps of small sub-batches), the partials summed in fixed order by a second kernel that
+   * runs the fused epilogue; NULL / too small: no split (same result up to the fp32 summation order) */
+  void* workspace;
+  int64_t workspace_bytes;
 } ydbl_conv_desc;
 int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream);
+int64_t ydbl_conv_workspace(const ydbl_conv_desc* d);
 
 /* DSConv in one kernel (conv.py:91-108): y = act(pw(dw(x)) + bias) [+ r], BN folded into pw.
  * dw_w fp32 [k*k][cin], pw_w [cout][kpad] in the view dtype (kpad = round_up(cin, 32), zero

@@ -81,6 +81,56 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin,cout,k,n,h,w,res", [
+    (768, 128, 3, 4, 20, 20, "add"),   # DBL-s head cv1 shape at a bs4 sub-batch (40^2 there): deep K, few tiles
+    (512, 64, 3, 2, 20, 20, None),     # Detect cv2 at P5 (DBL-s), 20^2
+    (1024, 256, 1, 4, 20, 20, "mul"),  # a deep-K 1x1
+])
+def test_conv_wsk_split_k(dtype, cin, cout, k, n, h, w, res):
+    """Wave-split-K with its k-loop split over workgroups (include/ydbl.h ydbl_conv_workspace: fp32 partial tiles,
+    summed in split order by the epilogue kernel): vs F.conv2d fp32, with the fused residual and the FullPAD second
+    output, and against the same conv without a workspace (unsplit) to fp32 summation-order rounding."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + cout + k)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, k, k) / (cin * k * k) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 1, k // 2))
+    outs = []
+    for split in (True, False):
+        plan = _plan(dtype)
+        xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+        yv = plan.alloc(n, h, w, cout + 8).cslice(0, cout)
+        rv, mode = None, _lib.RES_NONE
+        if res:
+            r = torch.randn(n, cout, h, w, generator=torch.Generator().manual_seed(5))
+            rv = _tv_from_nchw(plan, r)
+            mode = _lib.RES_ADD if res == "add" else _lib.RES_MUL
+        emit_dense(plan, xv, yv, wt, b, 1, k // 2, 1, _lib.ACT_SILU, rv, mode)
+        d = plan.steps[-1].args[0]
+        if split:
+            assert d.workspace and d.workspace_bytes == _lib.lib.ydbl_conv_workspace(d) > 0
+        else:
+            d.workspace, d.workspace_bytes = None, 0
+        r2 = torch.randn(n, cout, h, w, generator=torch.Generator().manual_seed(6))
+        r2v = _tv_from_nchw(plan, r2)
+        y2 = plan.alloc(n, h, w, cout)
+        assert plan.fuse_second_output(plan.writer_of(yv), y2, r2v, 0.5, 1.0) is not None
+        _run(plan)
+        outs.append((yv.nchw().float().cpu(), y2.nchw().float().cpu()))
+    want = ref
+    if res:
+        rr = r.to(dtype).float()
+        want = rr + ref if res == "add" else rr * ref
+    torch.testing.assert_close(outs[0][0], want, **_tol(dtype))
+    torch.testing.assert_close(outs[0][1], 0.5 * outs[0][0] + r2.to(dtype).float(), **_tol(dtype))
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(outs[0][0], outs[1][0], **tol)  # split vs unsplit: summation order only
+
+
 @pytest.mark.parametrize("cin,cout,n,h,w,res,second", [
     (128, 64, 32, 40, 40, None, False),    # DBL-n neck 1x1s at bs 32: two 16-px tiles per wave
     (64, 128, 32, 40, 40, "add", True),    # Cout 128: 128-wide column; residual + FullPAD second output

@@ -410,7 +410,11 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     biy[it] = (t % p.Ho) * p.S - p.PAD;
     bix[it] = ox * p.S - p.PAD;
   }
-  int cur_ci = kv * VEC, cur_kx = 0, cur_ky = 0;
+  // split-K: workgroup z of ksplit takes k-block steps [s0, s1) (ksplit 1: all of them)
+  const int nsteps_all = (p.K + BKB - 1) / BKB;
+  const int z = blockIdx.z;
+  const int s0 = (int)((int64_t)z * nsteps_all / p.ksplit), s1 = (int)((int64_t)(z + 1) * nsteps_all / p.ksplit);
+  int cur_ci = s0 * BKB + kv * VEC, cur_kx = 0, cur_ky = 0;
   if constexpr (!POINTWISE) {
     const int tap = cur_ci / p.Cin;
     cur_ci -= tap * p.Cin;
@@ -465,9 +469,10 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
 #pragma unroll
     for (int j = 0; j < TM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nsteps = (p.K + BKB - 1) / BKB;
+  // local step l = global step s0 + l (the loads past s1 are in bounds and never stored)
+  const int nsteps = s1 - s0;
 #pragma unroll
-  for (int u = 0; u < PF; ++u) load_step(u, ra[u], aok[u], rb[u], bok[u]);
+  for (int u = 0; u < PF; ++u) load_step(s0 + u, ra[u], aok[u], rb[u], bok[u]);
   store_step(0, ra[0], aok[0], rb[0], bok[0]);
   __syncthreads();
   const int myk = wave * 4 + g;  // k-vector this lane reads inside a block step
@@ -475,7 +480,7 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
       const int kb = k0 + u;
-      if (PF > 1 || kb + PF < nsteps) load_step(kb + PF, ra[u], aok[u], rb[u], bok[u]);
+      if (PF > 1 || kb + PF < nsteps) load_step(s0 + kb + PF, ra[u], aok[u], rb[u], bok[u]);
       if (kb < nsteps) {  // uniform
         const int buf = kb & 1;
         opv af[TN], bf[TM];
@@ -519,51 +524,112 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     const int64_t pp[1] = {m0 + j * 16 + r16};
     const bool pv[1] = {pp[0] < p.P};
     const int co[1] = {n0 + i * 16 + 4 * g};
-    conv_epilogue<T, 1, 1, Q8>(p, one, pp, pv, co);
+    if (p.ksplit > 1) {  // this split's partial tile, summed by splitk_epilogue_kernel (uniform branch)
+      if (pv[0] && co[0] < p.Cout)
+        *reinterpret_cast<f32x4*>(p.ws + ((int64_t)z * p.P + pp[0]) * ((p.Cout + 3) & ~3) + co[0]) = sum;
+    } else {
+      conv_epilogue<T, 1, 1, Q8>(p, one, pp, pv, co);
+    }
   }
+}
+
+// Split-K epilogue: one thread per (pixel, 4 output channels) sums the ksplit partial tiles in split order and runs
+// the same fused epilogue (bias, activation, residual, channel-slice store, second output) as the unsplit kernel.
+template <typename T, bool Q8>
+__global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs<T> p) {
+  const int c4 = (p.Cout + 3) >> 2, cs = c4 * 4;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t pix = t / c4;
+  const int co = (int)(t - pix * c4) * 4;
+  const bool ok = pix < p.P;
+  const int64_t pc = ok ? pix : 0;
+  f32x4 v[4];
+#pragma unroll
+  for (int z = 0; z < 4; ++z)  // all loads issued first (ksplit <= 4)
+    v[z] = z < p.ksplit ? *reinterpret_cast<const f32x4*>(p.ws + ((int64_t)z * p.P + pc) * cs + co) : f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 sum = v[0];
+#pragma unroll
+  for (int z = 1; z < 4; ++z)
+    if (z < p.ksplit) sum = f32x4{sum[0] + v[z][0], sum[1] + v[z][1], sum[2] + v[z][2], sum[3] + v[z][3]};
+  const f32x4 one[1][1] = {{sum}};
+  const int64_t pp[1] = {pix};
+  const bool pv[1] = {ok};
+  const int cc[1] = {co};
+  conv_epilogue<T, 1, 1, Q8>(p, one, pp, pv, cc);
+}
+
+// Split of the wave-split-K k-loop for a BM x BN tiling: the serial k-block chain is what a deep-K conv on a small
+// map waits on (DBL-s bs4 sub-batch: 768->128 3x3 @40^2, 400 tiles of 54 k-block steps, about 1 us each: 53.7 us in
+// graph), so below 768 tiles (3 workgroups per CU) the loop is split over up to 4 workgroups, each keeping >= 8
+// steps.  YDBL_SPLITK=0 (read per launch): no split (A/B switch).
+constexpr int WSK_SPLIT_BELOW = 768;
+template <typename T>
+static int wsk_ksplit(const ConvArgs<T>& a, int bm, int bn) {
+  const char* e = getenv("YDBL_SPLITK");
+  if (e && *e == '0') return 1;
+  const int64_t tiles = cdiv(a.P, bm) * cdiv(a.Cout, bn);
+  const int nsteps = (int)cdiv(a.K, 16 * Vec<T>::N);  // BKB
+  if (tiles >= WSK_SPLIT_BELOW || nsteps < 16) return 1;
+  int k = (int)std::min<int64_t>(4, (WSK_SPLIT_BELOW + tiles - 1) / tiles);
+  while (k > 1 && nsteps / k < 8) --k;
+  return k;
+}
+template <typename T>
+static int64_t wsk_ws_bytes(const ConvArgs<T>& a, int ksplit) {
+  return ksplit > 1 ? (int64_t)ksplit * a.P * ((a.Cout + 3) & ~3) * 4 : 0;
 }
 
 // Two k-block steps in flight (kbench bs16: 256->64 3x3 @20^2 18.8 -> 17.4 us; three or four: no better)
 constexpr int WSK_PF = 2;
 
 template <typename T, bool Q8, int BM, int BN>
-static void launch_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN));
+static void launch_wsk(const ConvArgs<T>& a0, bool pointwise, hipStream_t s) {
+  ConvArgs<T> a = a0;
+  a.ksplit = wsk_ksplit(a, BM, BN);
+  if (a.ksplit > 1 && (!a.ws || a.ws_bytes < wsk_ws_bytes(a, a.ksplit))) a.ksplit = 1;  // no room: unsplit
+  dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)a.ksplit);
   if (pointwise)
     conv_wsk_kernel<T, BM, BN, true, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
   else
     conv_wsk_kernel<T, BM, BN, false, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
+  if (a.ksplit > 1)
+    splitk_epilogue_kernel<T, Q8><<<(unsigned)cdiv((int64_t)a.P * ((a.Cout + 3) >> 2), 256), 256, 0, s>>>(a);
+}
+
+// The wave-split-K tiling try_wsk picks (BM, BN), without launching.
+template <typename T>
+static void wsk_tiles(const ConvArgs<T>& a, int& bm, int& bn) {
+  auto blocks = [&](int m, int n) { return cdiv(a.P, m) * cdiv(a.Cout, n); };
+  const int64_t want = 768;
+  if (a.Cout <= 128 && blocks(32, a.Cout <= 64 ? 64 : 128) < 256) { bm = a.Cout <= 64 ? 16 : 32; bn = 64; return; }
+  if (a.Cout <= 32) { bm = blocks(128, 32) >= want ? 128 : 64; bn = 32; return; }
+  if (a.Cout <= 64) { bm = blocks(64, 64) >= want ? 64 : 32; bn = 64; return; }
+  bm = 32;
+  bn = blocks(32, 128) >= want || a.Cout % 128 == 0 ? 128 : 64;
 }
 
 // Wave-split-K where the block-tiled GEMM runs out of parallelism or k-depth per barrier:
 // K >= 1024, or K >= 512 on small maps (measured on DBL-n: 384->64 3x3 @40^2 112 -> 82 us,
 // 256->64 3x3 @20^2 47 -> 27 us; 64->64 3x3 @80^2 stays on conv_igemm_kernel, 47 vs 74 us).
+template <typename T>
+static bool wsk_applies(const ConvArgs<T>& a) { return a.K >= 1024 || (a.K >= 512 && a.P <= 16384); }
+
 template <typename T, bool Q8>
 static bool try_wsk(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
-  if (!(a.K >= 1024 || (a.K >= 512 && a.P <= 16384))) return false;
-  auto blocks = [&](int bm, int bn) { return cdiv(a.P, bm) * cdiv(a.Cout, bn); };
-  const int64_t want = 768;
-  // Under 256 workgroups with the tiles below (the 20^2 maps of a bs16 sub-batch): half-height tiles, 16 pixels
-  // for Cout <= 64 and 64-wide columns for Cout 128 -- twice the workgroups for the same k-loop (bs16 graphs:
-  // 128->128 3x3 s2 @20^2 17.4 -> 14.4 us, 64->64 3x3 @20^2 9.5 -> 8.6, 256->64 18.4 -> 17.7; DBL-n bs32 even to
-  // +0.5 % over two boxes, DBL-s bs64 even: profiles/r04/r04_wsk_small_tiles_ab.txt)
-  if (a.Cout <= 128 && blocks(32, a.Cout <= 64 ? 64 : 128) < 256) {
-    if (a.Cout <= 64) launch_wsk<T, Q8, 16, 64>(a, pointwise, s);
-    else launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
-    return true;
-  }
-  if (a.Cout <= 32) {
-    if (blocks(128, 32) >= want) { launch_wsk<T, Q8, 128, 32>(a, pointwise, s); return true; }
-    launch_wsk<T, Q8, 64, 32>(a, pointwise, s);
-    return true;
-  }
-  if (a.Cout <= 64) {
-    if (blocks(64, 64) >= want) { launch_wsk<T, Q8, 64, 64>(a, pointwise, s); return true; }
-    launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
-    return true;
-  }
-  if (blocks(32, 128) >= want || a.Cout % 128 == 0) { launch_wsk<T, Q8, 32, 128>(a, pointwise, s); return true; }
-  launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
+  if (!wsk_applies(a)) return false;
+  // Tiles (wsk_tiles): under 256 workgroups with the usual tiles (the 20^2 maps of a bs16 sub-batch): half-height
+  // tiles, 16 pixels for Cout <= 64 and 64-wide columns for Cout 128 -- twice the workgroups for the same k-loop
+  // (bs16 graphs: 128->128 3x3 s2 @20^2 17.4 -> 14.4 us, 64->64 3x3 @20^2 9.5 -> 8.6, 256->64 18.4 -> 17.7; DBL-n
+  // bs32 even to +0.5 % over two boxes, DBL-s bs64 even: profiles/r04/r04_wsk_small_tiles_ab.txt); then the
+  // k-loop split where the tiles are still few (wsk_ksplit)
+  int bm, bn;
+  wsk_tiles(a, bm, bn);
+  if (bm == 16) launch_wsk<T, Q8, 16, 64>(a, pointwise, s);
+  else if (bm == 32 && bn == 64) launch_wsk<T, Q8, 32, 64>(a, pointwise, s);
+  else if (bm == 32) launch_wsk<T, Q8, 32, 128>(a, pointwise, s);
+  else if (bm == 64 && bn == 64) launch_wsk<T, Q8, 64, 64>(a, pointwise, s);
+  else if (bm == 64) launch_wsk<T, Q8, 64, 32>(a, pointwise, s);
+  else launch_wsk<T, Q8, 128, 32>(a, pointwise, s);
   return true;
 }
 
@@ -650,6 +716,8 @@ static ConvArgs<T> conv_args(const ydbl_conv_desc* d) {
   a.r2 = reinterpret_cast<const T*>(d->r2.ptr); a.r2cs = d->r2.cs;
   a.a2 = d->a2; a.b2 = d->b2;
   a.dq = d->dq; a.qs = d->qscale;
+  a.ws = reinterpret_cast<float*>(d->workspace); a.ws_bytes = d->workspace ? d->workspace_bytes : 0;
+  a.ksplit = 1;
   return a;
 }
 
@@ -710,4 +778,19 @@ extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
   if (const int rc = conv_check(d)) return rc;
   const hipStream_t s = as_stream(stream);
   return d->x.dtype == YDBL_F16 ? run_conv<_Float16>(d, s) : run_conv<float>(d, s);
+}
+
+// Split-K scratch the wave-split-K path would use for this descriptor (0: it would not split).  Computed as if the
+// conv took that path; a conv routed to another kernel ignores its workspace.
+template <typename T>
+static int64_t conv_ws_t(const ydbl_conv_desc* d) {
+  const ConvArgs<T> a = conv_args<T>(d);
+  if (!wsk_applies(a)) return 0;
+  int bm, bn;
+  wsk_tiles(a, bm, bn);
+  return wsk_ws_bytes(a, wsk_ksplit(a, bm, bn));
+}
+extern "C" int64_t ydbl_conv_workspace(const ydbl_conv_desc* d) {
+  if (conv_check(d)) return -1;
+  return d->x.dtype == YDBL_F16 ? conv_ws_t<_Float16>(d) : conv_ws_t<float>(d);
 }

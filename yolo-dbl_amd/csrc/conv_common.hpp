@@ -34,6 +34,9 @@ struct ConvArgs {
   const T* g0w; const float* g0b;
   const T* g0x; int g0xcs;
   T* g0y; int g0ycs; int g0act;
+  // split-K (conv_wsk_kernel): ksplit > 1 -> fp32 partial tiles ws[z][P][round_up(Cout, 4)], summed + epilogue by
+  // splitk_epilogue_kernel
+  float* ws; int64_t ws_bytes; int ksplit;
 };
 
 // ---- operand policy: f16/f32 vectors, or 8-byte groups of 8 e4m3 values (fp8 MFMA) -----------

@@ -31,7 +31,7 @@ class ConvDesc(C.Structure):
                 ("kh", C.c_int32), ("kw", C.c_int32), ("stride", C.c_int32), ("pad", C.c_int32), ("dil", C.c_int32),
                 ("kpad", C.c_int32), ("act", C.c_int32), ("res_mode", C.c_int32),
                 ("y2", View), ("r2", View), ("a2", C.c_float), ("b2", C.c_float),
-                ("dq", C.c_void_p), ("qscale", C.c_float)]
+                ("dq", C.c_void_p), ("qscale", C.c_float), ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64)]
 
 
 class DwConvDesc(C.Structure):
@@ -157,6 +157,7 @@ SIGNATURES = {
     "ydbl_detect_decode": ([C.POINTER(DecodeDesc), _P], C.c_int),
     "ydbl_pred_candidates": ([C.POINTER(PredCandDesc), _P], C.c_int),
     "ydbl_nms_workspace": ([C.c_int32, C.c_int32, C.c_int32], C.c_int64),
+    "ydbl_conv_workspace": ([C.POINTER(ConvDesc)], C.c_int64),
     "ydbl_nms": ([C.POINTER(NmsDesc), _P], C.c_int),
     "ydbl_conv_stem2_params_size": ([C.c_int32], C.c_int64),
     "ydbl_conv_stem2_pack": ([_P, _P, _P, _P, C.c_int32, _P], C.c_int),

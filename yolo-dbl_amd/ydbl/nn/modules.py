@@ -97,7 +97,13 @@ def emit_dense(plan: Plan, x: TV, y: TV, w: torch.Tensor, b: torch.Tensor | None
     d = ConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(), wd.data_ptr(),
                  bd.data_ptr() if bd is not None else None, kh, kw, stride, pad, dil, kpad, act, res_mode,
                  _null_view(), _null_view(), 0.0, 0.0, None, 1.0)
-    plan.launch("ydbl_conv2d_nhwc", d, what=what, keep=[wd, bd, d])
+    ws = None
+    if plan.device.type != "meta":  # split-K scratch of the deep-K small-map convs (include/ydbl.h ydbl_conv_workspace)
+        nws = int(_lib.lib.ydbl_conv_workspace(d))
+        if nws > 0:
+            ws = plan.splitk_scratch(nws)
+            d.workspace, d.workspace_bytes = ws.data_ptr(), nws
+    plan.launch("ydbl_conv2d_nhwc", d, what=what, keep=[wd, bd, d, ws])
     plan.note_writer(y, d)
     if plan.dtype == torch.float16 and x.c >= 64 and not what.startswith("Detect."):
         d._b32 = b.detach().float().cpu() if b is not None else None  # (ydbl.quant's bias correction)

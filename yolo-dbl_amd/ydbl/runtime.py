@@ -26,7 +26,7 @@ from ._lib import View, lib
 # routing in the C-ABI, read at build or at each launch).  tests/test_host_api.py checks this list against the
 # names the sources read.
 SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_HG_UNFUSED",
-            "YDBL_LSK_UNFUSED", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_NO_BNECK", "YDBL_NO_CV1_FUSE",
+            "YDBL_LSK_UNFUSED", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_SPLITK", "YDBL_NO_BNECK", "YDBL_NO_CV1_FUSE",
             "YDBL_NO_CV3_FUSE", "YDBL_NO_FUSE_PAD", "YDBL_NO_MERGE", "YDBL_NO_STEM2")
 
 
@@ -147,6 +147,15 @@ class Plan:
         self.buffers.append(t)
         self.bytes_allocated += t.numel()
         return t
+
+    def splitk_scratch(self, nbytes: int) -> torch.Tensor:
+        """fp32 partial tiles of a split-K conv (include/ydbl.h ydbl_conv_workspace).  One buffer serves every such
+        conv of the plan -- its launches run one after another on one stream -- and a larger need starts a larger
+        buffer (the earlier descriptors keep the one they were given)."""
+        cur = getattr(self, "_splitk", None)
+        if cur is None or cur.numel() < nbytes:
+            cur = self._splitk = self.scratch(nbytes)
+        return cur
 
     def const(self, t: torch.Tensor) -> torch.Tensor:
         t = t.detach().to(self.device).contiguous()
