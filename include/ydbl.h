@@ -173,7 +173,8 @@ int ydbl_dwconv2d_pair_nhwc(const ydbl_dwconv_desc* d0, const ydbl_dwconv_desc* 
  * without a staging copy).  When a kernel below gets a non-NULL `bind`, it takes the NCHW fp32 batch pointer from the
  * device word *bind->x (16-byte aligned, the same shape as x) and the scale from the device scalar *bind->amax, the
  * batch maximum, by LoadTensor's rule (U/data/loaders.py:561-566: x / 255 when max > 1 + FLT_EPSILON, else x; the
- * division is the multiply by fp32(1/255) that the GPU division computes) -- instead of x and scale. */
+ * division is the multiply by fp32(1/255) that the GPU division computes) -- instead of x and scale.  A record
+ * with both pointers NULL is no binding (x and scale are used); exactly one NULL is an error. */
 typedef struct {
   const float* const* x; /* device word holding the batch pointer */
   const float* amax;     /* device fp32 scalar: the batch maximum */

@@ -1,8 +1,7 @@
 #!/bin/bash
-# Round 6: NMS parity/timing + split-K conv parity and A/B (config 3 per-rank DBL-s bs8, config 2 DBL-n bs32).
+# Round 6: split-K conv parity and A/B (config 3 per-rank DBL-s bs8, config 2 DBL-n bs32) + bs4 layer profile.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; T=gpurun_out/r06_splitk; mkdir -p $T
 set -o pipefail
-bash scripts/gpu_r06_nms.sh || { echo "nms step failed"; tail -30 gpurun_out/r06_nms/pytest_nms.txt; exit 1; }
 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -x -q --timeout 120 --timeout-method thread \
     -k "conv_dense or split_k or conv1x1 or halo or vw" > $T/pytest_conv.txt 2>&1 || { tail -30 $T/pytest_conv.txt; exit 1; }
 timeout -k 10 300 python -u scripts/ab_bench.py "split:" "nosplit:YDBL_SPLITK=0" --model s --batch 8 --rounds 5 \

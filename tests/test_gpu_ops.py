@@ -83,13 +83,16 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("cin,cout,k,n,h,w,res", [
-    (768, 128, 3, 4, 20, 20, "add"),   # DBL-s head cv1 shape at a bs4 sub-batch (40^2 there): deep K, few tiles
+    (768, 128, 3, 4, 40, 40, "add"),   # DBL-s head 3x3 at a bs4 sub-batch: the halo kernel's split form
+    (384, 128, 3, 2, 40, 40, None),    # halo split form, 12 chunks
+    (768, 128, 3, 4, 20, 20, "add"),   # the same conv on 20^2: wave-split-K split
     (512, 64, 3, 2, 20, 20, None),     # Detect cv2 at P5 (DBL-s), 20^2
-    (1024, 256, 1, 4, 20, 20, "mul"),  # a deep-K 1x1
+    (2048, 256, 1, 4, 20, 20, "mul"),  # a deep-K 1x1
 ])
 def test_conv_wsk_split_k(dtype, cin, cout, k, n, h, w, res):
-    """Wave-split-K with its k-loop split over workgroups (include/ydbl.h ydbl_conv_workspace: fp32 partial tiles,
-    summed in split order by the epilogue kernel): vs F.conv2d fp32, with the fused residual and the FullPAD second
+    """Split-K convs (include/ydbl.h ydbl_conv_workspace: fp32 partial tiles summed in split order by the epilogue
+    kernel): the halo 3x3 kernel over input-channel chunks (small maps, >= 4096 output pixels) and the wave-split-K
+    kernel over k-block steps: vs F.conv2d fp32, with the fused residual and the FullPAD second
     output, and against the same conv without a workspace (unsplit) to fp32 summation-order rounding."""
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense

@@ -558,6 +558,14 @@ __global__ __launch_bounds__(256) void splitk_epilogue_kernel(ConvArgs<T> p) {
   conv_epilogue<T, 1, 1, Q8>(p, one, pp, pv, cc);
 }
 
+template <typename T, bool Q8>
+void launch_splitk_epilogue(const ConvArgs<T>& a, hipStream_t s) {
+  splitk_epilogue_kernel<T, Q8><<<(unsigned)cdiv((int64_t)a.P * ((a.Cout + 3) >> 2), 256), 256, 0, s>>>(a);
+}
+template void launch_splitk_epilogue<_Float16, false>(const ConvArgs<_Float16>&, hipStream_t);
+template void launch_splitk_epilogue<_Float16, true>(const ConvArgs<_Float16>&, hipStream_t);
+template void launch_splitk_epilogue<float, false>(const ConvArgs<float>&, hipStream_t);
+
 // Split of the wave-split-K k-loop for a BM x BN tiling: the serial k-block chain is what a deep-K conv on a small
 // map waits on (DBL-s bs4 sub-batch: 768->128 3x3 @40^2, 400 tiles of 54 k-block steps, about 1 us each: 53.7 us in
 // graph), so below 768 tiles (3 workgroups per CU) the loop is split over up to 4 workgroups, each keeping >= 8
@@ -592,8 +600,7 @@ static void launch_wsk(const ConvArgs<T>& a0, bool pointwise, hipStream_t s) {
     conv_wsk_kernel<T, BM, BN, true, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
   else
     conv_wsk_kernel<T, BM, BN, false, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
-  if (a.ksplit > 1)
-    splitk_epilogue_kernel<T, Q8><<<(unsigned)cdiv((int64_t)a.P * ((a.Cout + 3) >> 2), 256), 256, 0, s>>>(a);
+  if (a.ksplit > 1) launch_splitk_epilogue<T, Q8>(a, s);
 }
 
 // The wave-split-K tiling try_wsk picks (BM, BN), without launching.
@@ -688,6 +695,9 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
 }
 
 // Kernel choice: thin-input spatial tile (f16/f32 only), halo tile, wave-split-K, block GEMM.
+template <typename T>
+int halo_ksplit(const ConvArgs<T>& a, int64_t wgs);  // conv3x3.hip
+
 template <typename T, bool Q8>
 static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
   if constexpr (sizeof(T) == 2 && !Q8) {
@@ -785,10 +795,17 @@ extern "C" int ydbl_conv2d_nhwc(const ydbl_conv_desc* d, void* stream) {
 template <typename T>
 static int64_t conv_ws_t(const ydbl_conv_desc* d) {
   const ConvArgs<T> a = conv_args<T>(d);
-  if (!wsk_applies(a)) return 0;
-  int bm, bn;
-  wsk_tiles(a, bm, bn);
-  return wsk_ws_bytes(a, wsk_ksplit(a, bm, bn));
+  int64_t need = 0;
+  if (wsk_applies(a)) {
+    int bm, bn;
+    wsk_tiles(a, bm, bn);
+    need = wsk_ws_bytes(a, wsk_ksplit(a, bm, bn));
+  }
+  if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && (int64_t)a.P < 25600) {
+    const int64_t wgs = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * cdiv(a.Cout, 32);
+    need = std::max(need, wsk_ws_bytes(a, halo_ksplit(a, wgs)));
+  }
+  return need;
 }
 extern "C" int64_t ydbl_conv_workspace(const ydbl_conv_desc* d) {
   if (conv_check(d)) return -1;

@@ -16,6 +16,10 @@
 // bank quads for any starting pixel, and the mixed-g lane groups of ds_read_b128
 // ({0-3,12-15,20-27}, ...) stay conflict-free; weights are [co/16][tap][g][co%16] for the same
 // reason.  Fused epilogue (bias, SiLU, residual add, channel-slice store) from conv_common.hpp.
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "conv_common.hpp"
 
 namespace ydbl {
@@ -116,12 +120,16 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   // two k-steps per chunk, fewer barriers: 384->64 26.6 -> 28.2 us; timing split with the staging or the MFMAs
   // switched off: staging holds 24.7 of 26.6 us; an LDS-DMA chunk ring (buffer_load ... lds, 2-4 chunks in flight,
   // bit-identical) 26.4-27.1 us -- profiles/r05/r05_halo_*.txt)
-  const int nchunks = p.Cin / BK;
-  load_chunk(0);
+  // split-K (ksplit > 1, launch_halo): workgroup z of the tile takes input-channel chunks [c0, c1)
+  const int nchunks_all = p.Cin / BK;
+  const int z = blockIdx.y;
+  const int c0 = z * nchunks_all / p.ksplit, c1 = (z + 1) * nchunks_all / p.ksplit;
+  load_chunk(c0 * BK);
   store_chunk();
   bst.commit(s_bias);
   __syncthreads();
-  for (int ch = 0; ch < nchunks; ++ch) {
+  const int nchunks = c1;
+  for (int ch = c0; ch < nchunks; ++ch) {
     if (ch + 1 < nchunks) load_chunk((ch + 1) * BK);
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -158,13 +166,55 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   int co[NTN];
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
+  if (p.ksplit > 1) {  // this split's partial tile (f32), summed + epilogue by splitk_epilogue_kernel (conv.hip)
+    const int cs4 = (p.Cout + 3) & ~3;
+#pragma unroll
+    for (int j = 0; j < TMW; ++j)
+#pragma unroll
+      for (int i = 0; i < NTN; ++i)
+        if (pv[j] && co[i] < p.Cout) *reinterpret_cast<f32x4*>(p.ws + ((int64_t)z * p.P + pp[j]) * cs4 + co[i]) = acc[i][j];
+    return;
+  }
   conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co, s_bias, co0);
 }
 
+template <typename T, bool Q8>
+void launch_splitk_epilogue(const ConvArgs<T>& a, hipStream_t s);  // conv.hip
+
+// Split-K of the halo kernel for the deep-K stride-1 convs on small maps (fewer than 25600 output pixels: the 40^2
+// maps of a bs4 sub-batch), where a workgroup per tile leaves the chip idle behind a long serial chunk chain
+// (DBL-s 768->128 @40^2 bs4: 24 chunks; on the wave-split-K kernel it took 53.7 us, its 32-pixel tiles re-reading the
+// whole weight slice 200 times): up to 4 workgroups per tile over the input-channel chunks, >= 3 chunks each,
+// toward 512 workgroups; the partials summed in split order by the epilogue kernel.
+constexpr int HALO_SPLIT_MIN_CHUNKS = 8;
+template <typename T>
+int halo_ksplit(const ConvArgs<T>& a, int64_t wgs) {
+  const char* e = getenv("YDBL_SPLITK");
+  if ((e && *e == '0') || (int64_t)a.P >= 25600) return 1;
+  const int nch = a.Cin / (4 * Vec<T>::N);
+  if (nch < HALO_SPLIT_MIN_CHUNKS) return 1;
+  int k = (int)std::min<int64_t>(4, (512 + wgs - 1) / wgs);
+  while (k > 1 && nch / k < 3) --k;
+  return k;
+}
+
 template <typename T, bool Q8, int S, int TH>
-static void launch_halo(const ConvArgs<T>& a, hipStream_t s) {
+static void launch_halo(const ConvArgs<T>& a0, hipStream_t s) {
+  ConvArgs<T> a = a0;
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
+  a.ksplit = 1;
+  if (S == 1 && (int64_t)a.P < 25600) {  // (the split's own tiling: 32-channel slices below)
+    a.ksplit = halo_ksplit(a, ntiles * cdiv(a.Cout, 32));
+    if (a.ksplit > 1 && (!a.ws || a.ws_bytes < (int64_t)a.ksplit * a.P * ((a.Cout + 3) & ~3) * 4)) a.ksplit = 1;
+    if (a.ksplit > 1) {
+      const int cs = (int)cdiv(a.Cout, 32);
+      conv3x3_halo_kernel<T, S, TH, 2, Q8><<<dim3((unsigned)(ntiles * cs), (unsigned)a.ksplit), 256, 0, s>>>(
+          a, tiles_x, tiles_y, cs);
+      launch_splitk_epilogue<T, Q8>(a, s);
+      return;
+    }
+  }
   // Fewer than 400 64-channel workgroups (the 40^2 head convs of a bs16 sub-batch graph: 240) leave
   // most CUs with one workgroup; 32-channel slices double the grid (conv_bench.py bs16: 384->64 @40^2
   // 40.5 -> 29.5 us, 192->64 22.8 -> 17.3 us; at bs32, 480 workgroups, they lose: 49.2 -> 52.1 us)
@@ -206,7 +256,13 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   // 51200 output pixels (40^2 x 32) was the measured crossover at bs32; the bench's two bs16 sub-batch
   // graphs put the 40^2 head convs at 25600, where the halo tile still wins (DBL-n bs32 on two streams
   // 13.7 k -> 14.1 k img/s; 12800 loses again: 14.0 k)
-  if ((int64_t)a.P < 25600) return false;
+  if ((int64_t)a.P < 25600) {  // small maps: only as the split-K form (halo_ksplit), with room for its partials
+    const int64_t wgs = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * cdiv(a.Cout, 32);
+    const int k = halo_ksplit(a, wgs);
+    if (k < 2 || (int64_t)a.P < 4096 || !a.ws || a.ws_bytes < (int64_t)k * a.P * ((a.Cout + 3) & ~3) * 4) return false;
+    launch_halo<T, Q8, 1, 8>(a, s);
+    return true;
+  }
   const int64_t csplit = cdiv(a.Cout, 64);
   const int64_t tiles8 = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * csplit;
   const int64_t tiles16 = (int64_t)a.N * cdiv(a.Ho, 16) * cdiv(a.Wo, 16) * csplit;
@@ -357,6 +413,8 @@ bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
   return false;
 }
 
+template int halo_ksplit<_Float16>(const ConvArgs<_Float16>&, int64_t);
+template int halo_ksplit<float>(const ConvArgs<float>&, int64_t);
 template bool try_conv3x3_halo<_Float16, false>(const ConvArgs<_Float16>&, int, hipStream_t);
 template bool try_conv3x3_halo<_Float16, true>(const ConvArgs<_Float16>&, int, hipStream_t);
 template bool try_conv3x3_halo<float, false>(const ConvArgs<float>&, int, hipStream_t);

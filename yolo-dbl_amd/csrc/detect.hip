@@ -336,19 +336,19 @@ __device__ unsigned long long g_nms_stamps[16 * 4096];
 //                    original index) = its position in the reference's stable descending sort, summed over
 //                    column groups in a 64-bit accumulator whose last contribution writes order[rank] = slot;
 //   nms_mask_kernel  writes, in RANK space, row r word w bit s = IoU(rank r, rank 64w+s) > thr (torchvision's
-//                    decision, iou_gt) for the 64 x 64 blocks on and right of the diagonal (rows of
-//                    ceil(m / 64) words, packed per image).
+//                    decision, iou_gt), every word (the blocks right of the diagonal computed, the ones left of it
+//                    their mirror images; rows of ceil(m / 64) words, packed per image).
 // nms_kernel then sweeps the ranks in chunks of NMS_FAST: the chunk's rows are staged in LDS, and one wave walks
-// its 64-rank blocks in order -- a block is one mask word, so its live mask is ~(removed word) and its within-
-// block suppression words are the rows' diagonal words: a candidate is kept iff it is live and no kept
-// candidate earlier in its block suppresses it (the block greedy as the fixed point of K' = live & ~OR_{s in K}
-// D[s], one DPP wave-OR per step), and kept rows are ORed into the removed words.  Between chunks the new keeps'
-// rows are ORed, over the later ranks, into the image's removed bits.  Rows of earlier ranks would only set bits
-// whose decision is already made.
+// its 64-rank blocks in order, lane = rank.  A candidate is live iff no kept rank of an earlier chunk (the image's
+// removed bits) and no kept rank of an earlier block of the chunk suppresses it -- its own row's words ANDed with
+// the chunk's kept bits, one row read per lane whatever the number of keeps -- and it is kept iff it is live and no
+// kept candidate earlier in its block suppresses it (the rows' diagonal words; the block greedy as the fixed point
+// of K' = live & ~OR_{s in K} D[s], one DPP wave-OR per step).  Between chunks the new keeps' rows are ORed, over
+// the later ranks, into the image's removed bits.
 constexpr int NMS_FAST = 1024;        // ranks per sweep chunk (rows staged in LDS: 128 KiB)
 constexpr int NMS_FW = NMS_FAST / 64;  // 64-bit words per staged row
 constexpr int NMS_WIDE = 8192;         // candidates per image on this path (rank-space rows of 1 KiB)
-constexpr int NMS_RANK_COLS = 1024;    // columns per rank item of nms_pair_kernel (4 waves x 256)
+constexpr int NMS_RANK_COLS = 256;     // columns per rank item of nms_pair_kernel (4 waves x 64)
 
 // LDS slot of word w of staged row c: the words of a row are XOR-permuted by the row's low bits, so that
 // 64 lanes reading the same word of 64 different rows (the diagonal-word reads) spread over the banks, while
@@ -356,7 +356,8 @@ constexpr int NMS_RANK_COLS = 1024;    // columns per rank item of nms_pair_kern
 __device__ __forceinline__ int mslot(int c, int w) { return c * NMS_FW + (w ^ (c & (NMS_FW - 1))); }
 
 constexpr int NMS_PAIR_MAXB = 1024;  // images per launch on the pair-matrix path (block offsets in LDS)
-constexpr int NMS_PAIR_WGS = 512;    // workgroups of the two persistent chip-wide kernels
+constexpr int NMS_PAIR_WGS = 512;    // workgroups of the persistent rank kernel
+constexpr int NMS_MASK_WGS = 1024;   // and of the mask kernel (4 per CU: its blocks are short, latency-bound chains)
 
 // s_pre[b] = work items of images < b (wave 0 of a workgroup; items(n) per image)
 template <typename F>
@@ -394,12 +395,12 @@ __device__ __forceinline__ int nms_item_image(const int* s_pre, int nimg, int g)
   return lo;
 }
 
-// Rank items: 64 candidates (rows) against NMS_RANK_COLS columns, wave w taking 256 of them from LDS broadcasts;
+// Rank items: 64 candidates (rows) against NMS_RANK_COLS columns, wave w taking 64 of them as LDS broadcasts;
 // persistent over all images' items, so a heavy image's items spread over the whole chip.
 __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
   __shared__ int s_pre[NMS_PAIR_MAXB + 1];
   __shared__ int s_cnt[4][64];
-  __shared__ uint64_t s_ck[4][256];
+  __shared__ uint64_t s_ck[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   nms_item_prefix(p, nimg, s_pre, [](int nn) { return ((nn + 63) >> 6) * ((nn + NMS_RANK_COLS - 1) / NMS_RANK_COLS); });
   __syncthreads();
@@ -413,26 +414,21 @@ __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
     const int ng = (n + NMS_RANK_COLS - 1) / NMS_RANK_COLS;
     const int bi = t / ng, gq = t - bi * ng;
     const int i = bi * 64 + lane, ic = min(i, n - 1);
-    const int c0 = gq * NMS_RANK_COLS + wave * 256;
-    float csc[4];
-    int cix[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {  // this wave's 256 column keys (all loads issued first), then into LDS
-      const int jc = min(c0 + q * 64 + lane, n - 1);
-      csc[q] = sc[jc];
-      cix[q] = ix[jc];
-    }
-    const uint64_t ki = make_key(sc[ic], ix[ic]);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s_ck[wave][q * 64 + lane] = make_key(csc[q], cix[q]);
+    const int c0 = gq * NMS_RANK_COLS + wave * 64;
+    const int jc = min(c0 + lane, n - 1);
+    const float csc = sc[jc], isc = sc[ic];
+    const int cix = ix[jc], iix = ix[ic];
+    s_ck[wave][lane] = make_key(csc, cix);  // this wave's 64 column keys (wave-private)
+    const uint64_t ki = make_key(isc, iix);
     __builtin_amdgcn_wave_barrier();
-    const int ns = max(0, min(256, n - c0));  // wave-uniform
-    int below = 0, s = 0;
-    for (; s + 4 <= ns; s += 4) {
-      const uint64_t k0 = s_ck[wave][s], k1 = s_ck[wave][s + 1], k2 = s_ck[wave][s + 2], k3 = s_ck[wave][s + 3];
-      below += (k0 < ki) + (k1 < ki) + (k2 < ki) + (k3 < ki);
+    const int ns = max(0, min(64, n - c0));  // wave-uniform
+    int below = 0;
+    if (ns == 64) {
+#pragma unroll 16
+      for (int s = 0; s < 64; ++s) below += s_ck[wave][s] < ki;
+    } else {
+      for (int s = 0; s < ns; ++s) below += s_ck[wave][s] < ki;
     }
-    for (; s < ns; ++s) below += s_ck[wave][s] < ki;
     s_cnt[wave][lane] = below;
     __syncthreads();
     if (wave == 0 && i < n) {
@@ -449,12 +445,15 @@ __global__ __launch_bounds__(256) void nms_pair_kernel(NmsArgs p, int nimg) {
   }
 }
 
-// Rank-space IoU rows of the first m = min(n, max_nms) ranks, blocks on and right of the diagonal; each wave
-// takes one 64 x 64 block at a time (lane = row, the 64 columns as LDS broadcasts), no barrier.
+// Rank-space IoU rows of the first m = min(n, max_nms) ranks: a workgroup takes one 64 x 64 block on or right of the
+// diagonal at a time -- lane = row, wave w the block's columns 16w .. 16w+15 as LDS broadcasts -- and writes it AND,
+// from the same decisions gathered column by column (ballot), its mirror block left of the diagonal: every row
+// complete.  Persistent over all images' blocks.
 __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs p, int nimg) {
   __shared__ int s_pre[NMS_PAIR_MAXB + 1];
-  __shared__ f32x4 s_cb[4][64];
-  __shared__ float s_ca[4][64];
+  __shared__ f32x4 s_cb[4][16];
+  __shared__ float s_ca[4][16];
+  __shared__ uint64_t s_bits[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int mx = p.max_nms;
   nms_item_prefix(p, nimg, s_pre, [mx](int nn) {
@@ -463,7 +462,7 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs p, int nimg) {
   });
   __syncthreads();
   const int total = s_pre[nimg];
-  for (int g = blockIdx.x * 4 + wave; g < total; g += gridDim.x * 4) {
+  for (int g = blockIdx.x; g < total; g += gridDim.x) {
     const int b = nms_item_image(s_pre, nimg, g);
     const int n = min(p.ccount[b], p.cap);
     const int m = min(n, p.max_nms);
@@ -479,23 +478,34 @@ __global__ __launch_bounds__(256) void nms_mask_kernel(NmsArgs p, int nimg) {
     const float* cb = p.cbox + (int64_t)b * p.cap * 4;
     const int* cc = p.ccls + (int64_t)b * p.cap;
     const int* ord = p.worder + (int64_t)b * p.wrows;
-    const int r = bi * 64 + lane;
-    const int si = ord[min(r, m - 1)], sj = ord[min(bj * 64 + lane, m - 1)];
+    const int r = bi * 64 + lane, c = bj * 64 + 16 * wave + (lane & 15);
+    const int si = ord[min(r, m - 1)], sj = ord[min(c, m - 1)];
     const f32x4 vi = *reinterpret_cast<const f32x4*>(cb + (int64_t)si * 4);
     const f32x4 vj = *reinterpret_cast<const f32x4*>(cb + (int64_t)sj * 4);
     const float ci = float(cc[si]) * p.off_scale, cj = float(cc[sj]) * p.off_scale;  // boxes + cls * max_wh
     const f32x4 xi = f32x4{vi[0] + ci, vi[1] + ci, vi[2] + ci, vi[3] + ci};
     const f32x4 xj = f32x4{vj[0] + cj, vj[1] + cj, vj[2] + cj, vj[3] + cj};
     const float ai = (xi[2] - xi[0]) * (xi[3] - xi[1]);
-    s_cb[wave][lane] = xj;
-    s_ca[wave][lane] = (xj[2] - xj[0]) * (xj[3] - xj[1]);
+    if (lane < 16) {
+      s_cb[wave][lane] = xj;
+      s_ca[wave][lane] = (xj[2] - xj[0]) * (xj[3] - xj[1]);
+    }
     __builtin_amdgcn_wave_barrier();
-    const int ns = min(64, m - bj * 64);
-    uint64_t bits = 0;
-    for (int s = 0; s < ns; ++s)
-      if (iou_gt(xi, ai, s_cb[wave][s], s_ca[wave][s], p.th)) bits |= 1ull << s;
-    __builtin_amdgcn_wave_barrier();  // every lane's reads are done before the next block overwrites the columns
-    if (r < m) p.wmask[(int64_t)b * p.wrows * p.wwords + (int64_t)r * nbm + bj] = bits;  // rows of nbm words
+    const int ns = min(16, m - bj * 64 - 16 * wave);  // this wave's columns (may be <= 0)
+    uint64_t bits = 0, tw = 0;  // tw: lane s's transposed word = row (64 bj + 16 wave + s), word bi
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const bool hit = s < ns && r < m && iou_gt(xi, ai, s_cb[wave][s], s_ca[wave][s], p.th);
+      bits |= hit ? 1ull << (16 * wave + s) : 0ull;
+      const uint64_t col = __ballot(hit);  // the IoU is symmetric bit for bit: column s = row s of the twin block
+      tw = lane == s ? col : tw;
+    }
+    uint64_t* gm = p.wmask + (int64_t)b * p.wrows * p.wwords;  // rows of nbm words
+    if (bi < bj && lane < ns) gm[(int64_t)(bj * 64 + 16 * wave + lane) * nbm + bi] = tw;
+    s_bits[wave][lane] = bits;
+    __syncthreads();
+    if (wave == 0 && r < m) gm[(int64_t)r * nbm + bj] = s_bits[0][lane] | s_bits[1][lane] | s_bits[2][lane] | s_bits[3][lane];
+    __syncthreads();  // the columns and partial words are not overwritten before every wave is done with them
   }
 }
 
@@ -522,6 +532,7 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
   __shared__ float chunk_area[64];
   __shared__ unsigned char cmask[64][16];
   __shared__ int s_nk;
+  __shared__ uint64_t s_kb[NMS_FW];
   f32x4* s_box = reinterpret_cast<f32x4*>(s_keys);
   constexpr int LDS_BOXES = NMS_SORT_LDS * 8 / 16;
 
@@ -567,14 +578,13 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       const int nk_prev = s_nk;
       if (nk_prev >= p.max_det) break;
       const int L = min(NMS_FAST, m - R0), nbw = (L + 63) >> 6, w0 = R0 >> 6;
-      // (a) the chunk's rows, words of this chunk; rows of ranks an earlier chunk removed stay 0 (never read),
-      // and so do the words left of a row's own block (never written)
+      // (a) the chunk's rows, words of this chunk; rows of ranks an earlier chunk removed stay 0 (never read)
       {
         uint64_t v[NMS_FW];
 #pragma unroll
         for (int k = 0; k < NMS_FW; ++k) {
           const int e = t + k * NMS_THREADS, pos = e >> 4, w = e & (NMS_FW - 1), r = R0 + pos;
-          const bool ok = pos < L && w < nbw && w >= (pos >> 6) && !((wrem[min(r, m - 1) >> 6] >> (r & 63)) & 1ull);
+          const bool ok = pos < L && w < nbw && !((wrem[min(r, m - 1) >> 6] >> (r & 63)) & 1ull);
           v[k] = ok ? gm[(int64_t)r * W + w0 + w] : 0ull;
         }
 #pragma unroll
@@ -587,23 +597,34 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       NMS_TICK(ta);
       // (b) one wave sweeps the chunk's 64-rank blocks in order
       if (t < 64) {
-        uint64_t rem = lane < nbw ? wrem[w0 + lane] : ~0ull;  // lane w: removed flags of local ranks 64w .. 64w+63
+        const uint64_t xrem = lane < nbw ? wrem[w0 + lane] : ~0ull;  // lane w: removed by earlier chunks, word w
+        if (lane < NMS_FW) s_kb[lane] = 0ull;  // kept bits of the chunk's words (wave-private)
         int nk = nk_prev;
-        auto diag = [&](int blk) -> uint64_t {  // the lane's row, its own block's word
-          const int c = blk * 64 + lane;
-          return c < L ? smask[mslot(c, blk)] : 0ull;
+        auto row_of = [&](int blk, uint64_t (&rw)[NMS_FW]) {  // the lane's own row (rank 64 blk + lane), all words
+          const int c = min(blk * 64 + lane, L - 1);
+#pragma unroll
+          for (int w = 0; w < NMS_FW; ++w) rw[w] = smask[mslot(c, w)];
         };
-        uint64_t nx = diag(0);  // read one block ahead
+        uint64_t nrow[NMS_FW];
+        row_of(0, nrow);  // read one block ahead
         for (int blk = 0; blk < nbw && nk < p.max_det; ++blk) {
-          const uint64_t drow = nx;
-          if (blk + 1 < nbw) nx = diag(blk + 1);
+          uint64_t row[NMS_FW];
+#pragma unroll
+          for (int w = 0; w < NMS_FW; ++w) row[w] = nrow[w];
+          if (blk + 1 < nbw) row_of(blk + 1, nrow);
           const int cnt = min(64, L - blk * 64);
           const uint64_t valid = cnt == 64 ? ~0ull : ((1ull << cnt) - 1);
-          // (a bpermute, not v_readlane: a readlane of the 64-bit word with the loop's block index read the high
-          // half from another lane in this kernel -- the keep sets came out wrong)
-          const uint64_t rw = ((uint64_t)__shfl((uint32_t)(rem >> 32), blk) << 32) | __shfl((uint32_t)rem, blk);
-          const uint64_t M = valid & ~rw;  // live = not removed by a kept candidate of an earlier block
+          // removed by a kept rank of an earlier block of this chunk: the row's words AND the kept bits (s_kb of the
+          // words at and right of blk are still 0)
+          uint64_t sup = 0;
+#pragma unroll
+          for (int w = 0; w < NMS_FW; ++w) sup |= row[w] & s_kb[w];
+          const uint64_t rw = ((uint64_t)__shfl((uint32_t)(xrem >> 32), blk) << 32) | __shfl((uint32_t)xrem, blk);
+          const uint64_t M = valid & ~rw & ~__ballot(sup != 0);
           if (!M) continue;
+          uint64_t drow = row[0];  // the own block's word (blk is wave-uniform)
+#pragma unroll
+          for (int w = 1; w < NMS_FW; ++w) drow = w == blk ? row[w] : drow;
           const uint64_t dw = lane < 63 ? drow & (~0ull << (lane + 1)) : 0ull;  // later ranks of the block it suppresses
           const int nk0 = nk;
           // greedy inside the block: K_r = M_r & !(any s < r in K with D[s] bit r).  Iterated from K = M as
@@ -617,41 +638,11 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
             if (Kn == K) break;
             K = Kn;
           }
-#ifdef YDBL_NMS_DUMP
-          if (blockIdx.x == 1 && R0 == 0 && blk == 4) {
-            g_nms_stamps[2000 + lane] = drow;
-            g_nms_stamps[2100 + lane] = dw;
-            if (lane == 0) { g_nms_stamps[2200] = M; g_nms_stamps[2201] = K; g_nms_stamps[2202] = rw; g_nms_stamps[2203] = nk0; }
-          }
-#endif
           // keep[:max_det]: the greedy stops at max_det keeps, i.e. the lowest ranks of K
           for (int extra = __popcll(K) - (p.max_det - nk0); extra > 0; --extra) K &= ~(1ull << (63 - __clzll(K)));
           nk = nk0 + __popcll(K);
           if ((K >> lane) & 1) kept_slot[nk0 + __popcll(K & ((1ull << lane) - 1))] = R0 + blk * 64 + lane;  // a rank
-          // the kept candidates' rows join the removed flags (16 row reads in flight at a time; branch-free: all
-          // 16 reads are issued before the first OR)
-          while (K) {
-            int c[16];
-            bool ok[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-              const int tt = __ffsll((long long)K) - 1;  // -1 once K is empty
-              K &= K - 1;
-              ok[q] = tt >= 0;
-              c[q] = blk * 64 + (tt & 63);
-            }
-            uint64_t row[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) row[q] = smask[mslot(c[q], lane & (NMS_FW - 1))];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) rem |= ok[q] && lane < nbw ? row[q] : 0ull;
-          }
-#ifdef YDBL_NMS_DUMP
-          if (blockIdx.x == 1 && R0 == 0 && blk < 5) {
-            if (lane < 16) g_nms_stamps[3000 + blk * 16 + lane] = rem;
-            if (lane == 0) { g_nms_stamps[3100 + blk] = M; g_nms_stamps[3110 + blk] = rw; }
-          }
-#endif
+          if (lane == 0) s_kb[blk] = K;
         }
         if (lane == 0) s_nk = nk;
       }
@@ -1200,7 +1191,7 @@ extern "C" int ydbl_nms(const ydbl_nms_desc* d, void* stream) {
   a.fast = !(fe && *fe == '0') && d->n <= NMS_PAIR_MAXB;
   if (a.fast) {
     nms_pair_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
-    nms_mask_kernel<<<NMS_PAIR_WGS, 256, 0, s>>>(a, d->n);
+    nms_mask_kernel<<<NMS_MASK_WGS, 256, 0, s>>>(a, d->n);
   }
   // class-split sweep + merge (non-agnostic); the one-workgroup-per-image form for agnostic NMS or on request
   const char* ev = getenv("YDBL_NMS_GROUPS");  // A/B switch (read per launch: tests): 0 = one workgroup per image

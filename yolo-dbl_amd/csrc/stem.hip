@@ -165,7 +165,7 @@ using namespace ydbl;
 extern "C" int ydbl_conv_stem(const float* x, int32_t n, int32_t cin, int32_t h, int32_t w, float scale,
                               const float* wt, const float* bias, int32_t k, int32_t stride, int32_t act,
                               const ydbl_view* y, const ydbl_input_bind* bind, void* stream) {
-  if (bind && (!bind->x || !bind->amax)) return fail(YDBL_EINVAL, "stem: input binding with a null pointer");
+  if (bind && !bind->x != !bind->amax) return fail(YDBL_EINVAL, "stem: input binding with a null pointer");
   if (!x || !wt || !bias) return fail(YDBL_EINVAL, "stem: null input/weights");
   if (check_view(y, "stem.y", true)) return YDBL_EINVAL;
   if (cin != 3) return fail(YDBL_EINVAL, "stem: cin must be 3 (RGB; K = 27 = one MFMA k-step)");
