@@ -99,7 +99,7 @@ typedef struct {
    * dequantizes the fp32 accumulator before bias and activation. */
   const float* dq;
   float qscale;
-  /* optional split-K scratch (fp32 partial tiles): workspace_bytes >= ydbl_conv_workspace(d) lets the deep-K
+  /* optional split-K scratch (fp32 partial tiles; f16 convs only): workspace_bytes >= ydbl_conv_workspace(d) lets the deep-K
    * wave-split-K path split its k-loop over up to 4 workgroups per tile when the map gives too few tiles to fill the
    * chip (the 20^2 / 40^2 maps of small sub-batches), the partials summed in fixed order by a second kernel that
    * runs the fused epilogue; NULL / too small: no split (same result up to the fp32 summation order) */
