@@ -2,7 +2,7 @@
 # Round 6: the full GPU suite, then bench lines + rocprofv3 summaries of configs 2 (session and predict), 3 and 4.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; export TMPDIR=/tmp; T=gpurun_out/r06_full; mkdir -p $T
 set -o pipefail
-timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $T/pytest_gpu.txt 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread > $T/pytest_gpu.txt 2>&1 \
     || { tail -40 $T/pytest_gpu.txt; exit 1; }
 tail -2 $T/pytest_gpu.txt
 run() {  # name, bench args...

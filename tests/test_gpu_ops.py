@@ -81,7 +81,7 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
     torch.testing.assert_close(yv.nchw().float().cpu(), ref, **_tol(dtype))
 
 
-@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("dtype", [torch.float16])  # (the fp32 parity mode does not split)
 @pytest.mark.parametrize("cin,cout,k,n,h,w,res", [
     (768, 128, 3, 4, 40, 40, "add"),   # DBL-s head 3x3 at a bs4 sub-batch: the halo kernel's split form
     (384, 128, 3, 2, 40, 40, None),    # halo split form, 12 chunks
@@ -130,8 +130,7 @@ def test_conv_wsk_split_k(dtype, cin, cout, k, n, h, w, res):
         want = rr + ref if res == "add" else rr * ref
     torch.testing.assert_close(outs[0][0], want, **_tol(dtype))
     torch.testing.assert_close(outs[0][1], 0.5 * outs[0][0] + r2.to(dtype).float(), **_tol(dtype))
-    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
-    torch.testing.assert_close(outs[0][0], outs[1][0], **tol)  # split vs unsplit: summation order only
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-2, atol=1e-2)  # split vs unsplit: summation order
 
 
 @pytest.mark.parametrize("cin,cout,n,h,w,res,second", [

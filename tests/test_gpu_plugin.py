@@ -152,8 +152,8 @@ def _plugin_model(golden_dir, monkeypatch):
 
 def test_forward_only_plugin_eager_default_stream(golden_dir, monkeypatch):
     """use_graph=False runs the plan eagerly on torch's current stream -- the default (null) stream here, whose
-    handle is 0: the plugin step must run on it, bit-equal to the captured run of the same session
-    layout."""
+    handle is 0: the plugin step must run on it and agree with the captured run of the same session
+    layout (the plugin's torch convs may pick another MIOpen algorithm eagerly than under capture: not bit-equal)."""
     from ydbl.utils.synthetic import blob_images
 
     q = _plugin_model(golden_dir, monkeypatch)
@@ -164,7 +164,8 @@ def test_forward_only_plugin_eager_default_stream(golden_dir, monkeypatch):
     sg = q.session(2, 160, 160, half=False, conf=0.05, keep_pred=True, use_graph=True)
     sg(x)
     torch.cuda.synchronize()
-    assert torch.equal(se.pred, sg.pred)
+    d = (se.pred - sg.pred).abs()
+    assert d[:, :4].max().item() < 1e-2 and d[:, 4:].max().item() < 1e-4, d.max().item()
 
 
 def test_forward_only_plugin_fp8_calibration(golden_dir, monkeypatch):

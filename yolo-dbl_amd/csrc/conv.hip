@@ -362,7 +362,7 @@ static bool try_tile(const ConvArgs<T>& a, int kh, hipStream_t s) {
 // tiles are summed through LDS in fixed wave order before the fused epilogue.
 // LDS rows are 16 vectors (4*BK elements), slot-swizzled with (kv ^ row) so both the staging
 // stores and the 16x16 fragment reads are bank-conflict-free.
-template <typename T, int BM, int BN, bool POINTWISE, bool Q8, int PF = 1>
+template <typename T, int BM, int BN, bool POINTWISE, bool Q8, int PF = 1, bool SPLIT = false>
 __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
   constexpr int VEC = Vec<T>::N;
   constexpr int BK = 4 * VEC;    // per wave
@@ -411,9 +411,12 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     bix[it] = ox * p.S - p.PAD;
   }
   // split-K: workgroup z of ksplit takes k-block steps [s0, s1) (ksplit 1: all of them)
+  // (a template flag: the runtime start step cost the unsplit kernels up to 86 VGPRs -- 2 -> 1 waves per SIMD on
+  // the 32 x 128 tiles, DBL-l 1280's deep 3x3s 142 -> 272 us)
   const int nsteps_all = (p.K + BKB - 1) / BKB;
-  const int z = blockIdx.z;
-  const int s0 = (int)((int64_t)z * nsteps_all / p.ksplit), s1 = (int)((int64_t)(z + 1) * nsteps_all / p.ksplit);
+  const int z = SPLIT ? (int)blockIdx.z : 0;
+  const int s0 = SPLIT ? (int)((int64_t)z * nsteps_all / p.ksplit) : 0;
+  const int s1 = SPLIT ? (int)((int64_t)(z + 1) * nsteps_all / p.ksplit) : nsteps_all;
   int cur_ci = s0 * BKB + kv * VEC, cur_kx = 0, cur_ky = 0;
   if constexpr (!POINTWISE) {
     const int tap = cur_ci / p.Cin;
@@ -524,7 +527,7 @@ __global__ __launch_bounds__(256) void conv_wsk_kernel(ConvArgs<T> p) {
     const int64_t pp[1] = {m0 + j * 16 + r16};
     const bool pv[1] = {pp[0] < p.P};
     const int co[1] = {n0 + i * 16 + 4 * g};
-    if (p.ksplit > 1) {  // this split's partial tile, summed by splitk_epilogue_kernel (uniform branch)
+    if constexpr (SPLIT) {  // this split's partial tile, summed by splitk_epilogue_kernel
       if (pv[0] && co[0] < p.Cout)
         *reinterpret_cast<f32x4*>(p.ws + ((int64_t)z * p.P + pp[0]) * ((p.Cout + 3) & ~3) + co[0]) = sum;
     } else {
@@ -574,7 +577,7 @@ constexpr int WSK_SPLIT_BELOW = 768;
 template <typename T>
 static int wsk_ksplit(const ConvArgs<T>& a, int bm, int bn) {
   const char* e = getenv("YDBL_SPLITK");
-  if (e && *e == '0') return 1;
+  if (sizeof(T) != 2 || (e && *e == '0')) return 1;  // fp16 only: the fp32 parity mode keeps one summation order
   const int64_t tiles = cdiv(a.P, bm) * cdiv(a.Cout, bn);
   const int nsteps = (int)cdiv(a.K, 16 * Vec<T>::N);  // BKB
   if (tiles >= WSK_SPLIT_BELOW || nsteps < 16) return 1;
@@ -596,11 +599,15 @@ static void launch_wsk(const ConvArgs<T>& a0, bool pointwise, hipStream_t s) {
   a.ksplit = wsk_ksplit(a, BM, BN);
   if (a.ksplit > 1 && (!a.ws || a.ws_bytes < wsk_ws_bytes(a, a.ksplit))) a.ksplit = 1;  // no room: unsplit
   dim3 grid((unsigned)cdiv(a.P, BM), (unsigned)cdiv(a.Cout, BN), (unsigned)a.ksplit);
-  if (pointwise)
+  if (a.ksplit > 1) {
+    if (pointwise) conv_wsk_kernel<T, BM, BN, true, Q8, WSK_PF, true><<<grid, 256, 0, s>>>(a);
+    else conv_wsk_kernel<T, BM, BN, false, Q8, WSK_PF, true><<<grid, 256, 0, s>>>(a);
+    launch_splitk_epilogue<T, Q8>(a, s);
+  } else if (pointwise) {
     conv_wsk_kernel<T, BM, BN, true, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
-  else
+  } else {
     conv_wsk_kernel<T, BM, BN, false, Q8, WSK_PF><<<grid, 256, 0, s>>>(a);
-  if (a.ksplit > 1) launch_splitk_epilogue<T, Q8>(a, s);
+  }
 }
 
 // The wave-split-K tiling try_wsk picks (BM, BN), without launching.

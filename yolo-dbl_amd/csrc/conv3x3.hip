@@ -190,7 +190,7 @@ constexpr int HALO_SPLIT_MIN_CHUNKS = 8;
 template <typename T>
 int halo_ksplit(const ConvArgs<T>& a, int64_t wgs) {
   const char* e = getenv("YDBL_SPLITK");
-  if ((e && *e == '0') || (int64_t)a.P >= 25600) return 1;
+  if (sizeof(T) != 2 || (e && *e == '0') || (int64_t)a.P >= 25600) return 1;  // fp16 only (conv.hip wsk_ksplit)
   const int nch = a.Cin / (4 * Vec<T>::N);
   if (nch < HALO_SPLIT_MIN_CHUNKS) return 1;
   int k = (int)std::min<int64_t>(4, (512 + wgs - 1) / wgs);

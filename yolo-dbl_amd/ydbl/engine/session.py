@@ -107,7 +107,9 @@ class DetectSession:
         self._bound = None  # the last tensor launch_bound() read (introspection)
         self._calls, self._slot_ptrs, self._pgraph, self._pout, self._pheld = 0, {}, {}, {}, {}
         self._max_work = {}  # per binding slot: the batch-max kernel's tickets are reset by its last block
-        self._last_ev = None  # the last launch_bound() replay: the slots share the plans' activation buffers
+        # the last launch_bound() replay (the slots share the plans' activation buffers): its stream and, per slot, an
+        # event recorded after it -- a call from another stream waits for it, detach() waits for its slot's
+        self._last_stream, self._slot_ev = None, {}
         if _outputs is None and gather_rows is not None:
             # one record per image [det (max_det*6 fp32) | count (int32) | pad]: the boxes and counts of a batch-
             # sharded predict leave the GPU in ONE all-gather (ydbl.parallel); rows >= batch stay empty padding
@@ -299,12 +301,14 @@ class DetectSession:
             self._set_slot(0)
             self._pgraph[k] = g
         cur = torch.cuda.current_stream(dev)
-        if self._last_ev is not None:  # a replay issued from another stream must finish first (shared activations)
-            cur.wait_event(self._last_ev)
+        if self._last_stream is not None and cur != self._last_stream:  # another stream: the last replay first
+            cur.wait_event(self._slot_ev[1 + self._calls % 2])  # (the other slot's event: the previous call)
         g.replay()
-        ev = torch.cuda.Event()
+        ev = self._slot_ev.get(k)
+        if ev is None:
+            ev = self._slot_ev[k] = torch.cuda.Event()
         ev.record(cur)
-        self._last_ev = ev
+        self._last_stream = cur
         det, count, flat, scale = self._pout[k]
         out = BoundOutputs(det, count, flat, scale, ev)
         self._pheld[k] = weakref.ref(out)
