@@ -11,3 +11,5 @@ for cfg in "c2:--model n" "c2p:--model n --via-predict" "c3:--model s --batch 8"
   timeout -k 10 300 python bench.py $a --no-cpu-baseline --no-roofline > $T/$n.log 2>&1 || { echo "bench $n failed"; exit 1; }
   python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(sys.argv[2], d['value'], d['ms_per_step'])" $T/$n.log $n
 done
+timeout -k 10 400 python -u scripts/val_timing.py > $T/val_timing.txt 2>&1 || { tail -20 $T/val_timing.txt; exit 1; }
+tail -6 $T/val_timing.txt

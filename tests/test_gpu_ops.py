@@ -133,6 +133,45 @@ def test_conv_wsk_split_k(dtype, cin, cout, k, n, h, w, res):
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-2, atol=1e-2)  # split vs unsplit: summation order
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin,cout,n,h,w,res", [
+    (128, 256, 4, 40, 40, "add"),  # DBL-s bs4 head 3x3: unsplittable (4 chunks), Cout 256 -> halo tile, 32-ch slices
+    (64, 128, 3, 37, 41, None),    # ragged map, 2 chunks
+    (192, 160, 2, 48, 48, "mul"),  # Cout tail of a 32-channel slice
+])
+def test_conv3x3_halo_small_map(monkeypatch, dtype, cin, cout, n, h, w, res):
+    """Small maps (4096..25599 output pixels) with too few input-channel chunks to split and Cout >= 128 take the
+    halo tile instead of the wave-split-K kernel (conv3x3.hip try_conv3x3_halo): vs F.conv2d fp32, and against
+    the wave-split-K route (YDBL_HALO_SMALL=0) to summation-order rounding."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + cout)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 1, 1))
+    r = torch.randn(n, cout, h, w, generator=torch.Generator().manual_seed(5)) if res else None
+    if res:
+        rr = r.to(dtype).float()
+        ref = rr + ref if res == "add" else rr * ref
+    outs = []
+    for route in ("1", "0"):
+        monkeypatch.setenv("YDBL_HALO_SMALL", route)
+        plan = _plan(dtype)
+        xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+        yv = plan.alloc(n, h, w, cout + 8).cslice(8, cout)
+        rv = _tv_from_nchw(plan, r) if res else None
+        mode = {None: _lib.RES_NONE, "add": _lib.RES_ADD, "mul": _lib.RES_MUL}[res]
+        emit_dense(plan, xv, yv, wt, b, 1, 1, 1, _lib.ACT_SILU, rv, mode)
+        _run(plan)
+        outs.append(yv.nchw().float().cpu())
+    torch.testing.assert_close(outs[0], ref, **_tol(dtype))
+    torch.testing.assert_close(outs[1], ref, **_tol(dtype))
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(outs[0], outs[1], **tol)
+
+
 @pytest.mark.parametrize("cin,cout,n,h,w,res,second", [
     (128, 64, 32, 40, 40, None, False),    # DBL-n neck 1x1s at bs 32: two 16-px tiles per wave
     (64, 128, 32, 40, 40, "add", True),    # Cout 128: 128-wide column; residual + FullPAD second output

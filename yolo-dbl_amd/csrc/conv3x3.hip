@@ -259,9 +259,15 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   if ((int64_t)a.P < 25600) {  // small maps: only as the split-K form (halo_ksplit), with room for its partials
     const int64_t wgs = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * cdiv(a.Cout, 32);
     const int k = halo_ksplit(a, wgs);
-    if (k < 2 || (int64_t)a.P < 4096 || !a.ws || a.ws_bytes < (int64_t)k * a.P * ((a.Cout + 3) & ~3) * 4) return false;
-    launch_halo<T, Q8, 1, 8>(a, s);
-    return true;
+    if ((int64_t)a.P < 4096) return false;
+    if (k >= 2 && a.ws && a.ws_bytes >= (int64_t)k * a.P * ((a.Cout + 3) & ~3) * 4) return launch_halo<T, Q8, 1, 8>(a, s), true;
+    // Too few chunks to split (Cin < 256) and wide Cout: the wave-split-K kernel's 32x128 tiles would re-read the
+    // whole weight matrix once per 32 pixels (DBL-s bs4: 128->256 @40^2, 200 tile rows x 590 KB); the halo tile in
+    // 32-channel slices reads it once per 128 pixels
+    // (YDBL_HALO_SMALL=0, read per launch: the wave-split-K route, A/B switch)
+    const char* e = getenv("YDBL_HALO_SMALL");
+    if (k < 2 && a.Cout >= 128 && !(e && *e == '0')) return launch_halo<T, Q8, 1, 8>(a, s), true;
+    return false;
   }
   const int64_t csplit = cdiv(a.Cout, 64);
   const int64_t tiles8 = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * csplit;
