@@ -75,7 +75,10 @@ cases = [("DBL-s bs4: 1188,900,700,500", [1188, 900, 700, 500], 3, 8400, 640),
          ("DBL-l bs4: 6210,4000,3000,2000", [6210, 4000, 3000, 2000], 3, 33600, 1280),
          ("4 x 6210", [6210] * 4, 3, 33600, 1280),
          ("1 x 8192", [8192], 1, 33600, 1280),
-         ("DBL-n bs16: 16 x 640", [640] * 16, 3, 8400, 640)]
+         ("DBL-n bs16: 16 x 640", [640] * 16, 3, 8400, 640),
+         # above 8192 candidates both columns run the select path (nms_select_sort): 3 buckets, and > max_nms 30000
+         ("4 x 20000", [20000] * 4, 1, 33600, 1280),
+         ("4 x 33600 (> max_nms)", [33600] * 4, 1, 33600, 1280)]
 if len(sys.argv) > 1:  # one case under a profiler: python scripts/nms_wide_bench.py <case> <per_image> <wide>
     label, counts, nc, A, size = cases[int(sys.argv[1])]
     os.environ["YDBL_NMS_FAST"] = sys.argv[3]

@@ -1054,6 +1054,12 @@ def _rand_pred(n, nc, A, seed, ties=False):
     dict(nc=1, A=2000, conf=0.0, iou=0.0, multi=False),             # iou 0 on the wide path
     dict(nc=3, A=4000, conf=0.0, iou=0.7, multi=False, max_det=700),  # max_det reached in a later chunk
     dict(nc=4, A=9000, conf=0.0, iou=0.7, multi=True),  # 36000 candidates > max_nms 30000: stable truncation
+    # > 8192 candidates: radix select of the first max_nms keys, 8192-key buckets sorted in LDS (nms_select_sort)
+    dict(nc=80, A=3000, conf=0.001, iou=0.7, multi=True),              # 240000 candidates, 4 buckets
+    dict(nc=80, A=3000, conf=0.001, iou=0.6, multi=True, ties=True),   # 240000, 8 score levels: index order decides
+    dict(nc=10, A=2000, conf=0.0, iou=0.7, multi=True, max_nms=8192),  # 20000 -> exactly one full bucket
+    dict(nc=5, A=2000, conf=0.0, iou=0.7, multi=True, max_nms=32768),  # 10000 < max_nms: every key, 2 buckets
+    dict(nc=1, A=30000, conf=0.0, iou=0.95, multi=False, max_det=4096, max_nms=24577),  # bucket 4: one key
 ])
 @pytest.mark.parametrize("groups", ["1", "0"])
 @pytest.mark.parametrize("fast", ["1", "0"])

@@ -7,8 +7,9 @@
 //          gives the reference (anchor order, or torch.where's (anchor, class) row-major order).
 // nms    : images with <= 8192 candidates: chip-wide ranks (= the stable sort's positions) and rank-space
 //          IoU > thr bit rows, then one 1024-thread workgroup per image sweeps 64-rank blocks (the pair-matrix
-//          path below); larger images: per-image bitonic key/value sort and a chunked greedy sweep with the
-//          suppression flags and the first 4096 sorted boxes in LDS.  Both stop after max_det keeps, which is
+//          path below); larger images: a per-image radix select of the first max_nms sort keys, sorted in
+//          8192-key buckets in LDS (nms_select_sort), and a chunked greedy sweep with the suppression flags and
+//          the first 4096 sorted boxes in LDS.  Both stop after max_det keeps, which is
 //          the reference's keep[:max_det] because keeps are produced in score order.
 #include <stdlib.h>
 
@@ -294,6 +295,174 @@ __device__ void reg_bitonic(uint64_t& key, int& val, int P, uint64_t* xk, int* x
         }
       }
     }
+  }
+}
+
+// Images above NMS_SORT_LDS candidates (validation settings: conf 0.001, multi-label; the reference truncates to
+// argsort(descending)[:max_nms]): the first m = min(n, max_nms) sorted (key, slot) pairs into gk / gv[0, m), by one
+// workgroup and without sorting the n candidates.
+//   1. radix select, 8 bits per pass from the top of the 64-bit key, for the bucket targets t_j = min(8192 (j+1), m):
+//      per pass, an LDS histogram of the keys that share target j's prefix; the bin where the running count reaches
+//      the target's remaining rank extends the prefix.  A target is resolved when its rank is the last of its bin
+//      (bound U_j = prefix with all lower bits set: exactly t_j keys are <= U_j) or after the 8th pass (the key);
+//   2. one pass scatters every key <= U_{nb-1} into bucket j (the first j with key <= U_j) at gk[8192 j + ...];
+//   3. each bucket (<= 8192 pairs, key range (U_{j-1}, U_j]) is sorted in LDS and written back in place, which is
+//      its final position since bucket j starts at rank t_{j-1} = 8192 j.
+// Keys are unique (they carry the candidate's original index), so the m pairs and their order are those of the
+// reference's stable sort.  Passes read the n scores and indices (8 B per candidate); DBL-l 1280 nc80 at conf 0.001
+// with 2.6 M candidates per image: 3-4 passes.  (Before: one bitonic sort of next_pow2(n) pairs in global memory,
+// 62 ms per image at that size.)
+constexpr int NMS_BUCKETS = NMS_MAX_FLAGS / NMS_SORT_LDS;
+constexpr int SEL_U = 2;  // candidates in flight per thread and pass
+
+__device__ void nms_select_sort(const float* sc, const int* ix, int n, int m, uint64_t* gk, int* gv, uint64_t* s_keys,
+                                int* s_vals, int* hist /* LDS, NMS_BUCKETS x 256 */) {
+  __shared__ uint64_t s_pre[NMS_BUCKETS], s_ub[NMS_BUCKETS];
+  __shared__ int s_need[NMS_BUCKETS], s_done[NMS_BUCKETS], s_cnt[NMS_BUCKETS];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  const int nb = (m + NMS_SORT_LDS - 1) / NMS_SORT_LDS;
+  if (t < nb) {
+    s_pre[t] = 0;
+    s_need[t] = min(NMS_SORT_LDS * (t + 1), m);  // 1-based rank of the target within its prefix group
+    s_done[t] = t == nb - 1 && m == n;             // every key: no bound needed
+    s_ub[t] = ~0ull;
+    s_cnt[t] = 0;
+  }
+  __syncthreads();
+  for (int d = 0; d < 8; ++d) {
+    bool open = false;
+    for (int j = 0; j < nb; ++j) open |= !s_done[j];
+    if (!open) break;
+    const int sh = 56 - 8 * d;
+    for (int i = t; i < nb * 256; i += NMS_THREADS) hist[i] = 0;
+    // targets that share a prefix share the histogram: only the first of each prefix (src) counts
+    uint64_t pre[NMS_BUCKETS];
+    bool opn[NMS_BUCKETS], act[NMS_BUCKETS];
+    int src[NMS_BUCKETS];
+#pragma unroll
+    for (int j = 0; j < NMS_BUCKETS; ++j) {
+      pre[j] = s_pre[j];
+      opn[j] = j < nb && !s_done[j];
+      src[j] = j;
+#pragma unroll
+      for (int q = j - 1; q >= 0; --q)
+        if (opn[q] && pre[q] == pre[j]) src[j] = q;
+      act[j] = opn[j] && src[j] == j;
+    }
+    __syncthreads();
+    // keys crowd into few bins in the first passes (scores share their exponent): up to two rounds of one
+    // aggregated LDS add per distinct bin of the wave, then per-lane adds for the rest
+    for (int i0 = t; i0 - lane < n; i0 += SEL_U * NMS_THREADS) {
+      uint64_t key[SEL_U];
+#pragma unroll
+      for (int u = 0; u < SEL_U; ++u) {
+        const int i = i0 + u * NMS_THREADS;
+        key[u] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < SEL_U; ++u) {
+        const bool valid = i0 + u * NMS_THREADS < n;
+        const int dig = (int)((key[u] >> sh) & 255);
+        const uint64_t kp = d == 0 ? 0ull : key[u] >> (sh + 8);
+#pragma unroll
+        for (int j = 0; j < NMS_BUCKETS; ++j) {
+          if (!act[j]) continue;  // wave-uniform
+          bool pend = valid && kp == pre[j];
+#pragma unroll
+          for (int r = 0; r < 2; ++r) {
+            const uint64_t mm = __ballot(pend);
+            if (!mm) break;
+            const int leader = __ffsll((long long)mm) - 1;
+            const int ld = __shfl(dig, leader);
+            const uint64_t same = __ballot(pend && dig == ld);
+            if (lane == leader) atomicAdd(&hist[j * 256 + ld], __popcll(same));
+            pend = pend && dig != ld;
+          }
+          if (pend) atomicAdd(&hist[j * 256 + dig], 1);
+        }
+      }
+    }
+    __syncthreads();
+    if (wave < nb && opn[wave]) {  // wave j resolves target j: lane l holds bins 4l .. 4l+3
+      const int j = wave;
+      int hs = j;  // the first open target with this prefix counted the histogram
+#pragma unroll
+      for (int q = 0; q < NMS_BUCKETS; ++q) hs = q == j ? src[q] : hs;
+      int c[4], sum = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) sum += (c[q] = hist[hs * 256 + 4 * lane + q]);
+      int incl = sum;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      const int need = s_need[j];
+      int before = incl - sum;
+      if (before < need && need <= incl) {  // exactly one lane
+        int q = 3, cq = c[3];  // the first bin of the lane where the count reaches need (unrolled: no scratch)
+#pragma unroll
+        for (int u = 2; u >= 0; --u) {
+          int b4 = before;
+#pragma unroll
+          for (int v = 0; v <= u; ++v) b4 += c[v];
+          if (b4 >= need) { q = u; cq = c[u]; }
+        }
+#pragma unroll
+        for (int v = 0; v < 3; ++v) before += v < q ? c[v] : 0;
+        const uint64_t pre2 = (s_pre[j] << 8) | (uint64_t)(4 * lane + q);
+        const int need2 = need - before;
+        s_pre[j] = pre2;
+        s_need[j] = need2;
+        if (need2 == cq || d == 7) {
+          s_done[j] = 1;
+          s_ub[j] = sh == 0 ? pre2 : ((pre2 << sh) | ((1ull << sh) - 1));
+        }
+      }
+    }
+    __syncthreads();
+  }
+  // 2. scatter into the buckets
+  uint64_t ub[NMS_BUCKETS];
+#pragma unroll
+  for (int j = 0; j < NMS_BUCKETS; ++j) ub[j] = j < nb ? s_ub[j] : 0ull;
+  for (int i0 = t - lane; i0 < n; i0 += NMS_THREADS) {  // wave-uniform trip count: one LDS add per bucket and wave
+    const int i = i0 + lane;
+    const uint64_t key = i < n ? make_key(sc[i], ix[i]) : ~0ull;
+    const bool sel = i < n && key <= ub[nb - 1];
+    int j = 0;
+#pragma unroll
+    for (int q = 0; q < NMS_BUCKETS - 1; ++q) j += q < nb - 1 && key > ub[q];
+    int pos = 0;
+#pragma unroll
+    for (int q = 0; q < NMS_BUCKETS; ++q) {
+      const uint64_t mm = __ballot(sel && j == q);
+      if (!mm) continue;
+      const int leader = __ffsll((long long)mm) - 1;
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&s_cnt[q], __popcll(mm));
+      base = __shfl(base, leader);
+      if (sel && j == q) pos = NMS_SORT_LDS * q + base + __popcll(mm & ((1ull << lane) - 1));
+    }
+    if (sel) {
+      gk[pos] = key;
+      gv[pos] = i;
+    }
+  }
+  __syncthreads();
+  // 3. sort each bucket in LDS, in place
+  for (int j = 0; j < nb; ++j) {
+    const int c = s_cnt[j], base = NMS_SORT_LDS * j;
+    int P = 64;
+    while (P < c) P <<= 1;
+    for (int i = t; i < P; i += NMS_THREADS) {
+      s_keys[i] = i < c ? gk[base + i] : ~0ull;
+      s_vals[i] = i < c ? gv[base + i] : -1;
+    }
+    __syncthreads();
+    block_bitonic(s_keys, s_vals, P);
+    for (int i = t; i < c; i += NMS_THREADS) gv[base + i] = s_vals[i];
+    __syncthreads();
   }
 }
 
@@ -738,15 +907,10 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsArgs p) {
       __syncthreads();
       if (n > 1) block_bitonic(s_keys, s_vals, P);
       order = s_vals;
-    } else {
-      uint64_t* gk = p.gkeys + (int64_t)b * p.L;
+    } else {  // the first min(n, max_nms) of the sorted order only (nms_select_sort)
       int* gv = p.gvals + (int64_t)b * p.L;
-      for (int i = threadIdx.x; i < P; i += NMS_THREADS) {
-        gk[i] = i < n ? make_key(sc[i], ix[i]) : ~0ull;
-        gv[i] = i < n ? i : -1;
-      }
-      __syncthreads();
-      block_bitonic(gk, gv, P);
+      nms_select_sort(sc, ix, n, min(n, p.max_nms), p.gkeys + (int64_t)b * p.L, gv, s_keys, s_vals,
+                      reinterpret_cast<int*>(removed));
       order = gv;
     }
     const int m = min(n, p.max_nms);
@@ -1127,7 +1291,8 @@ extern "C" int ydbl_pred_candidates(const ydbl_pred_cand_desc* d, void* stream) 
 
 // [global sort keys n*L x 8 B][sort slots n*L x 4 B][group keys n*G*gk x 8 B][group slots x 4 B][counts n*G x 4 B]
 // [pad to 8 B][rank accumulators n*R x 8 B][rank-space rows n*R x R/64 x 8 B][order n*R x 4 B]
-static int64_t nms_sort_len(int32_t cap) { return cap <= NMS_SORT_LDS ? 0 : next_pow2(cap); }
+// (bucket space of nms_select_sort: the first max_nms <= NMS_MAX_FLAGS sorted pairs, in 8192-pair buckets)
+static int64_t nms_sort_len(int32_t cap) { return cap <= NMS_SORT_LDS ? 0 : std::min(next_pow2(cap), NMS_MAX_FLAGS); }
 static int32_t nms_group_len(int32_t cap) { return cap < NMS_MAX_DET ? cap : NMS_MAX_DET; }
 // rows per image of the pair-matrix path: candidates up to NMS_WIDE, in whole 64-row blocks
 static int32_t nms_rank_rows(int32_t cap) { return (std::min(cap, NMS_WIDE) + 63) / 64 * 64; }
