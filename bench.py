@@ -57,10 +57,7 @@ def conv_traffic(step, elsize):
 
 def dsconv_traffic(step, elsize):
     """ydbl_dsconv_nhwc: x read, y written (+ residual, + the fused class-conv output), dw + pw weights."""
-    return _dsconv_bytes(step.args[0], elsize)
-
-
-def _dsconv_bytes(d, elsize):
+    d = step.args[0]
     x, y = d.x, d.y
     byts = (_px(x) * x.c + _px(y) * y.c) * elsize + x.c * d.k * d.k * 4 + y.c * x.c * elsize
     if d.res_mode:
@@ -173,19 +170,7 @@ def lsk_traffic(step, elsize):
     return 3 * p * dim * elsize, 2.0 * p * (dim // 2) * dim + 2.0 * p * 98 * 2
 
 
-def dsb_traffic(step, elsize):
-    """ydbl_dsbottleneck_nhwc: the two DSConvs' bytes less the intermediate's round trip (it stays on chip) and the
-    residual re-read (the first DSConv's input, already read)."""
-    d1, d2 = step.args[0], step.args[1]
-    (b1, f1), (b2, f2) = _dsconv_bytes(d1, elsize), _dsconv_bytes(d2, elsize)
-    byts = b1 + b2 - 2 * _px(d1.y) * d1.y.c * elsize
-    if d2.res_mode:
-        byts -= _px(d2.y) * d2.y.c * elsize
-    return byts, f1 + f2
-
-
 TRAFFIC = {"ydbl_conv2d_nhwc": ("conv2d", conv_traffic), "ydbl_dsconv_nhwc": ("dsconv", dsconv_traffic),
-           "ydbl_dsbottleneck_nhwc": ("dsconv", dsb_traffic),
            "ydbl_dysample2": ("dysample", dysample2_traffic), "ydbl_hg_fused": ("hypergraph", hg_fused_traffic),
            "ydbl_bottleneck_nhwc": ("bottleneck", bneck_traffic), "ydbl_conv_stem2": ("stem2", stem2_traffic),
            "ydbl_dysample_ex": ("dysample", dysample_traffic), "ydbl_lsk_attn": ("lsk", lsk_traffic),

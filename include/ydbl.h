@@ -152,14 +152,6 @@ typedef struct {
 } ydbl_dsconv_desc;
 int ydbl_dsconv_nhwc(const ydbl_dsconv_desc* d, void* stream);
 
-/* DSBottleneck (nn/modules/block.py:1408-1444: y = [x +] DSConv_k2(DSConv_k1(x))) as one call: d1 = the k1 DSConv
- * (x -> t, optionally with the leading 1x1 g0), d2 = the k2 DSConv (d2.x == d1.y == t, residual d2.r == d1.x or none,
- * optionally with the trailing GEMM g2).  Replaces the two ydbl_dsconv_nhwc calls DSBottleneck.forward makes
- * (block.py:1442-1444; cv1 / cv2 of conv.py:91-108).  Where fp16, 64 channels, k1 = 3 and k2 = 7 (stride 1, DSC3k2's
- * blocks): one launch with the intermediate t in LDS (its 3-px halo recomputed; t itself is NOT written),
- * bit-identical to the two launches; otherwise exactly those two launches. */
-int ydbl_dsbottleneck_nhwc(const ydbl_dsconv_desc* d1, const ydbl_dsconv_desc* d2, void* stream);
-
 /* Depthwise convolution (groups = C), fp32 arithmetic.
  * y = act(dwconv(x, w) + bias), then res_mode ADD: y = r + y (GhostBottleneck identity shortcut).
  * w: fp32 [kh][kw][c]; bias: fp32 [c] or NULL; r: view or ignored. */

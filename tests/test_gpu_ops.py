@@ -88,13 +88,11 @@ def test_conv_dense(dtype, cin, cout, k, s, act, res):
     (768, 128, 3, 4, 20, 20, "add"),   # the same conv on 20^2: wave-split-K split
     (512, 64, 3, 2, 20, 20, None),     # Detect cv2 at P5 (DBL-s), 20^2
     (2048, 256, 1, 4, 20, 20, "mul"),  # a deep-K 1x1
-    (384, 64, 3, 16, 40, 40, "add"),   # DBL-n head 3x3 at a bs16 sub-batch (25600 px): the larger-map split, 3 ways
-    (256, 32, 3, 16, 80, 80, None),    # DBL-n 256->32 @80^2 bs16 (102400 px): larger-map split, 2 ways
 ])
 def test_conv_wsk_split_k(dtype, cin, cout, k, n, h, w, res):
     """Split-K convs (include/ydbl.h ydbl_conv_workspace: fp32 partial tiles summed in split order by the epilogue
     kernel): the halo 3x3 kernel over input-channel chunks (small maps, >= 4096 output pixels) and the wave-split-K
-    kernel over k-block steps, and the halo kernel's larger-map form (25600 <= P < 204800): vs F.conv2d fp32, with the fused residual and the FullPAD second
+    kernel over k-block steps: vs F.conv2d fp32, with the fused residual and the FullPAD second
     output, and against the same conv without a workspace (unsplit) to fp32 summation-order rounding."""
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense
@@ -1174,7 +1172,6 @@ def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
     x = torch.randn(*shape)
     outs, nsteps = [], []
     monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")  # the leading-1x1 fusion has its own test (below)
-    monkeypatch.setenv("YDBL_DSB_PAIR", "0")  # the one-launch bottleneck has its own test (test_dsb_pair_bit_identical)
     for fuse in ("1", ""):
         if fuse:
             monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
@@ -1198,83 +1195,6 @@ def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
     torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
 
 
-@pytest.mark.parametrize("n,shape,sliced,cv1,cv3", [
-    (2, (16, 64, 40, 40), False, True, True),   # DBL-n's DSC3k at a bs16 sub-batch: g0 on the first pair, g2 on the last
-    (1, (3, 64, 13, 21), True, True, True),     # one bottleneck: g0 and g2 in the same launch; ragged map
-    (2, (2, 64, 9, 7), True, False, False),     # plain pairs; map smaller than the 16x16 halo
-    (2, (5, 64, 20, 20), False, False, True),
-    (2, (2, 64, 24, 17), True, True, False),
-    (2, (4, 128, 40, 40), True, False, True),   # DBL-s's DSC3k at config 3's bs4 sub-batch: 128 channels, 8 waves
-    (2, (3, 128, 20, 20), False, False, False),
-])
-def test_dsb_pair_bit_identical(n, shape, sliced, cv1, cv3, monkeypatch):
-    """DSBottleneck (U/nn/modules/block.py:1408-1444) as ONE ydbl_dsbottleneck_nhwc launch (csrc/dsb_pair.hip: the
-    k3 DSConv's output kept in LDS with its 3-px halo recomputed, the residual from the staged input), inside DSC3k
-    (block.py:1447-1503) with and without the leading / trailing 1x1s riding on it == the two ydbl_dsconv_nhwc launches
-    per bottleneck (YDBL_DSB_PAIR=0), bit for bit, every output the block writes; one launch per bottleneck fewer;
-    close to the oracle."""
-    from oracle import model as om
-    from ydbl.nn import modules as M
-    from ydbl.utils.synthetic import trained_like_
-
-    c = shape[1]
-    torch.manual_seed(n + shape[2] + shape[3])
-    o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=11).eval()
-    x = torch.randn(*shape)
-    if not cv1:
-        monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")
-    if not cv3:
-        monkeypatch.setenv("YDBL_NO_CV3_FUSE", "1")
-    outs, nsteps = [], []
-    for pair in ("1", "0"):
-        monkeypatch.setenv("YDBL_DSB_PAIR", pair)
-        pm = M.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7)
-        pm.load_state_dict(o.state_dict())
-        plan = _plan(torch.float16)
-        xv = _tv_from_nchw(plan, x)
-        ybuf = plan.alloc(shape[0], shape[2], shape[3], c + (24 if sliced else 0))
-        yv = ybuf.cslice(8, c) if sliced else ybuf
-        pm.emit(plan, xv, yv)
-        names = [st.fn.__name__ for st in plan.steps]
-        nsteps.append(len(names))
-        assert names.count("ydbl_dsbottleneck_nhwc") == (n if pair == "1" else 0), names
-        _run(plan)
-        outs.append(yv.nchw().float().cpu())
-    assert nsteps[0] == nsteps[1] - n
-    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
-    with torch.no_grad():
-        ref = o(x)
-    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
-
-
-@pytest.mark.parametrize("shape,add,x_sliced", [((4, 64, 40, 40), True, True), ((3, 64, 11, 29), False, False)])
-def test_dsb_pair_standalone(shape, add, x_sliced, monkeypatch):
-    """A lone DSBottleneck (C2f's m when DSC3k2 has dsc3k=False), with and without its shortcut and reading a channel
-    slice: the one-launch pair == the two DSConv launches bit for bit, close to the oracle."""
-    from oracle import model as om
-    from ydbl.nn import modules as M
-    from ydbl.utils.synthetic import trained_like_
-
-    torch.manual_seed(shape[2])
-    o = trained_like_(om.DSBottleneck(64, 64, shortcut=add, e=1.0, k1=3, k2=7), seed=3).eval()
-    x = torch.randn(*shape)
-    outs = []
-    for pair in ("1", "0"):
-        monkeypatch.setenv("YDBL_DSB_PAIR", pair)
-        pm = M.DSBottleneck(64, 64, shortcut=add, e=1.0, k1=3, k2=7)
-        pm.load_state_dict(o.state_dict())
-        plan = _plan(torch.float16)
-        xv = _tv_from_nchw(plan, x, cs_extra=16, c_off=8) if x_sliced else _tv_from_nchw(plan, x)
-        yv = pm.emit(plan, xv)
-        assert [st.fn.__name__ for st in plan.steps].count("ydbl_dsbottleneck_nhwc") == (pair == "1")
-        _run(plan)
-        outs.append(yv.nchw().float().cpu())
-    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
-    with torch.no_grad():
-        ref = o(x)
-    torch.testing.assert_close(outs[0], ref, rtol=3e-2, atol=3e-2)
-
-
 @pytest.mark.parametrize("n,shape,sliced", [(2, (16, 64, 40, 40), False), (1, (3, 64, 13, 21), True),
                                             (2, (2, 64, 9, 7), True)])
 def test_dsc3k_cv1_fused_bit_identical(n, shape, sliced, monkeypatch):
@@ -1290,7 +1210,6 @@ def test_dsc3k_cv1_fused_bit_identical(n, shape, sliced, monkeypatch):
     o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=7).eval()
     x = torch.randn(*shape)
     outs, nsteps = [], []
-    monkeypatch.setenv("YDBL_DSB_PAIR", "0")  # the one-launch bottleneck has its own test (test_dsb_pair_bit_identical)
     for fuse in ("1", ""):
         if fuse:
             monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)

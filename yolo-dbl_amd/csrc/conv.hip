@@ -704,8 +704,6 @@ static void dispatch_conv(const ConvArgs<T>& a, bool pointwise, hipStream_t s) {
 // Kernel choice: thin-input spatial tile (f16/f32 only), halo tile, wave-split-K, block GEMM.
 template <typename T>
 int halo_ksplit(const ConvArgs<T>& a, int64_t wgs);  // conv3x3.hip
-template <typename T>
-int halo_ksplit_big(const ConvArgs<T>& a, int64_t wgs);  // conv3x3.hip
 
 template <typename T, bool Q8>
 static void route(const ConvArgs<T>& a, int kh, bool pw, hipStream_t s) {
@@ -810,10 +808,9 @@ static int64_t conv_ws_t(const ydbl_conv_desc* d) {
     wsk_tiles(a, bm, bn);
     need = wsk_ws_bytes(a, wsk_ksplit(a, bm, bn));
   }
-  if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && (int64_t)a.P < 204800) {
+  if (d->kh == 3 && d->kw == 3 && d->stride == 1 && d->pad == 1 && d->dil == 1 && (int64_t)a.P < 25600) {
     const int64_t wgs = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * cdiv(a.Cout, 32);
     need = std::max(need, wsk_ws_bytes(a, halo_ksplit(a, wgs)));
-    need = std::max(need, wsk_ws_bytes(a, halo_ksplit_big(a, wgs)));
   }
   return need;
 }

@@ -198,38 +198,12 @@ int halo_ksplit(const ConvArgs<T>& a, int64_t wgs) {
   return k;
 }
 
-// Split-K on the larger maps too (25600 <= P < 204800: the 40^2 / 80^2 deep-K head convs of the bench's bs16 sub-batch
-// graphs, e.g. DBL-n 384->64 @40^2, 12 chunks per tile): the same split form toward 1024 workgroups.
-// YDBL_SPLITK_BIG=0 (read per launch): no split there (A/B switch).
-template <typename T>
-int halo_ksplit_big(const ConvArgs<T>& a, int64_t wgs) {
-  const char* e = getenv("YDBL_SPLITK_BIG");
-  const char* e2 = getenv("YDBL_SPLITK");
-  if (sizeof(T) != 2 || (e && *e == '0') || (e2 && *e2 == '0') || (int64_t)a.P < 25600 || (int64_t)a.P >= 204800) return 1;
-  const int nch = a.Cin / (4 * Vec<T>::N);
-  if (nch < HALO_SPLIT_MIN_CHUNKS) return 1;
-  int k = (int)std::min<int64_t>(4, (1024 + wgs - 1) / wgs);
-  while (k > 1 && nch / k < 4) --k;
-  return k;
-}
-
 template <typename T, bool Q8, int S, int TH>
 static void launch_halo(const ConvArgs<T>& a0, hipStream_t s) {
   ConvArgs<T> a = a0;
   const int tiles_x = (int)cdiv(a.Wo, 16), tiles_y = (int)cdiv(a.Ho, TH);
   const int64_t ntiles = (int64_t)a.N * tiles_y * tiles_x;
   a.ksplit = 1;
-  if (S == 1 && TH == 8 && (int64_t)a.P >= 25600) {  // larger maps: 32-channel slices, the split toward 1024 workgroups
-    a.ksplit = halo_ksplit_big(a, ntiles * cdiv(a.Cout, 32));
-    if (a.ksplit > 1 && (!a.ws || a.ws_bytes < (int64_t)a.ksplit * a.P * ((a.Cout + 3) & ~3) * 4)) a.ksplit = 1;
-    if (a.ksplit > 1) {
-      const int cs = (int)cdiv(a.Cout, 32);
-      conv3x3_halo_kernel<T, S, TH, 2, Q8><<<dim3((unsigned)(ntiles * cs), (unsigned)a.ksplit), 256, 0, s>>>(
-          a, tiles_x, tiles_y, cs);
-      launch_splitk_epilogue<T, Q8>(a, s);
-      return;
-    }
-  }
   if (S == 1 && (int64_t)a.P < 25600) {  // (the split's own tiling: 32-channel slices below)
     a.ksplit = halo_ksplit(a, ntiles * cdiv(a.Cout, 32));
     if (a.ksplit > 1 && (!a.ws || a.ws_bytes < (int64_t)a.ksplit * a.P * ((a.Cout + 3) & ~3) * 4)) a.ksplit = 1;
@@ -305,11 +279,6 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   (void)tiles8;
   // Cout <= 32 (one 32-channel slice: the weights are as many bytes per chunk as the halo): 16-row tiles from
   // 256 of them (DBL-n's 256->32 @80^2 at bs16, 400 tiles: 34.6 -> 31.8 us in graph, scripts/kbench.py)
-  {
-    const int64_t wgs = (int64_t)a.N * cdiv(a.Ho, 8) * cdiv(a.Wo, 16) * cdiv(a.Cout, 32);
-    const int k = halo_ksplit_big(a, wgs);
-    if (k >= 2 && a.ws && a.ws_bytes >= (int64_t)k * a.P * ((a.Cout + 3) & ~3) * 4) return launch_halo<T, Q8, 1, 8>(a, s), true;
-  }
   if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256)) launch_halo<T, Q8, 1, 16>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);
   return true;
@@ -451,8 +420,6 @@ bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
 }
 
 template int halo_ksplit<_Float16>(const ConvArgs<_Float16>&, int64_t);
-template int halo_ksplit_big<_Float16>(const ConvArgs<_Float16>&, int64_t);
-template int halo_ksplit_big<float>(const ConvArgs<float>&, int64_t);
 template int halo_ksplit<float>(const ConvArgs<float>&, int64_t);
 template bool try_conv3x3_halo<_Float16, false>(const ConvArgs<_Float16>&, int, hipStream_t);
 template bool try_conv3x3_halo<_Float16, true>(const ConvArgs<_Float16>&, int, hipStream_t);

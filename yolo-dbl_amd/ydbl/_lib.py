@@ -132,7 +132,6 @@ SIGNATURES = {
     "ydbl_dwconv2d_nhwc": ([C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dwconv2d_pair_nhwc": ([C.POINTER(DwConvDesc), C.POINTER(DwConvDesc), _P], C.c_int),
     "ydbl_dsconv_nhwc": ([C.POINTER(DsConvDesc), _P], C.c_int),
-    "ydbl_dsbottleneck_nhwc": ([C.POINTER(DsConvDesc), C.POINTER(DsConvDesc), _P], C.c_int),
     "ydbl_batch_max_work_ints": ([], C.c_int32),
     "ydbl_batch_max_work_init": ([_P], None),
     "ydbl_batch_max": ([_P, C.c_int64, _P, _P, _P, _P], C.c_int),

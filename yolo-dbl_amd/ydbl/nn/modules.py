@@ -186,18 +186,7 @@ def emit_dsconv(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Te
                 act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv",
                 w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE,
                 tail: tuple | None = None, g2: tuple | None = None, g0: tuple | None = None) -> TV:
-    """One ydbl_dsconv_nhwc launch (dsconv_desc)."""
-    desc, keep, y, what = dsconv_desc(plan, dw, x, out, w_pw, b_pw, act, res, res_mode, what, w_dw, b_dw, dw_act,
-                                      tail, g2, g0)
-    plan.launch("ydbl_dsconv_nhwc", desc, what=what, keep=keep)
-    return y
-
-
-def dsconv_desc(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Tensor, b_pw: torch.Tensor,
-                act=_lib.ACT_SILU, res: TV | None = None, res_mode=_lib.RES_NONE, what="DSConv",
-                w_dw: torch.Tensor | None = None, b_dw: torch.Tensor | None = None, dw_act=_lib.ACT_NONE,
-                tail: tuple | None = None, g2: tuple | None = None, g0: tuple | None = None):
-    """(descriptor, tensors to keep alive, output view, launch name) of a DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA.
+    """DSConv (conv.py:91-108) as one ydbl_dsconv_nhwc launch: depthwise tile in LDS feeding the pw MFMA.
     w_dw / b_dw / dw_act: folded DWConv weights, bias and activation (Detect's DWConv -> Conv1x1 pair).
     tail = (w [n, co], b [n], out view): a trailing 1x1 conv with n <= 4 outputs in the same launch.
     g2 = (w [co2, co + c2] fp32, b [co2], x2 view, y2 view, act): a trailing GEMM over [y ; x2] into y2 (C3's
@@ -237,7 +226,9 @@ def dsconv_desc(plan: Plan, dw: nn.Conv2d, x: TV, out: TV | None, w_pw: torch.Te
     desc = _lib.DsConvDesc(x.struct(), y.struct(), res.struct() if res is not None else _null_view(),
                            dww.data_ptr(), pww.data_ptr(), bd.data_ptr(), k, st, p, d, kpad, act, res_mode,
                            dwb.data_ptr() if dwb is not None else None, dw_act, *tail_args, *g2_args, *g0_args)
-    return desc, [dww, pww, bd, dwb, tw, tb, g2w, g2b, g0w, g0b, desc], y, f"{what}.k{k}s{st}"
+    plan.launch("ydbl_dsconv_nhwc", desc, what=f"{what}.k{k}s{st}",
+                keep=[dww, pww, bd, dwb, tw, tb, g2w, g2b, g0w, g0b, desc])
+    return y
 
 
 def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = None, what="DWConv+Conv1x1",
@@ -797,47 +788,12 @@ class DSBottleneck(PlanModule):
         self.cv2 = DSConv(c_, c2, k2, s=1, p=None, d=d2)
         self.add = shortcut and c1 == c2
 
-    def pair_fusable(self, plan, x, pre=None) -> bool:
-        """Both DSConvs as one ydbl_dsbottleneck_nhwc launch (csrc/dsb_pair.hip): fp16, 64 channels in, between and
-        out (128 on maps of <= 160 8x8 tiles, without a leading 1x1), k3 then k7 (stride 1, no dilation), the library
-        switch on -- the library's own rule (it runs the same two launches otherwise)."""
-        d1, d2 = self.cv1.dw, self.cv2.dw
-        c = x.c
-        small = x.n * -(-x.h // 8) * -(-x.w // 8) <= 160
-        return (plan.dtype == torch.float16 and os.environ.get("YDBL_DSB_PAIR") != "0"
-                and os.environ.get("YDBL_DS_LEAN") != "0" and (c == 64 or (c == 128 and small and not pre))
-                and x.cs % 8 == 0
-                and d1.in_channels == self.cv1.pw.out_channels == d2.in_channels == self.cv2.pw.out_channels == c
-                and d1.kernel_size == (3, 3) and d1.stride == (1, 1) and d1.dilation == (1, 1) and d1.padding == (1, 1)
-                and d2.kernel_size == (7, 7) and d2.stride == (1, 1) and d2.dilation == (1, 1) and d2.padding == (3, 3)
-                and d1.bias is None and d2.bias is None)
-
     def emit(self, plan, x, out=None, cv3=None, pre=None):
         """cv3 = (C3's cv3 Conv, its second input view (the cv2 branch), its output view or None): the DSC3k's
         cv3 as the trailing GEMM of this bottleneck's k7 DSConv; returns cv3's output then.
         pre = (C3's cv2, cv1, their input, their [cv2 | cv1] output view whose last c_ channels are x): the merged
-        1x1 as the leading GEMM of this bottleneck's k3 DSConv (C3._cv1_fusable).
-        Both DSConvs as one launch where pair_fusable (the intermediate then never leaves the CU)."""
+        1x1 as the leading GEMM of this bottleneck's k3 DSConv (C3._cv1_fusable)."""
         y = out if out is not None else plan.alloc(x.n, x.h, x.w, self.cv2.pw.out_channels)
-        if self.pair_fusable(plan, x, pre):
-            g0 = None
-            if pre is not None:
-                c2m, c1m, x0, y0 = pre
-                (w2, b2), (w1, b1) = c2m.folded(), c1m.folded()
-                g0 = (torch.cat([w2, w1], 0).reshape(y0.c, x0.c), torch.cat([b2, b1], 0), x0, y0, _act_code(c1m.act))
-            w1p, b1p = fold_bn(self.cv1.pw.weight, self.cv1.pw.bias, self.cv1.bn)
-            d1, k1, t, n1 = dsconv_desc(plan, self.cv1.dw, x, None, w1p, b1p, _lib.ACT_SILU, g0=g0)
-            g2, o3 = None, None
-            if cv3 is not None:
-                conv3, x2, o3 = cv3
-                o3 = o3 if o3 is not None else plan.alloc(x.n, x.h, x.w, conv3.conv.out_channels)
-                w3, b3 = conv3.folded()
-                g2 = (w3.reshape(w3.shape[0], -1), b3, x2, o3, _act_code(conv3.act))
-            w2p, b2p = fold_bn(self.cv2.pw.weight, self.cv2.pw.bias, self.cv2.bn)
-            d2, k2, _, n2 = dsconv_desc(plan, self.cv2.dw, t, y, w2p, b2p, _lib.ACT_SILU, x if self.add else None,
-                                        _lib.RES_ADD if self.add else _lib.RES_NONE, g2=g2)
-            plan.launch("ydbl_dsbottleneck_nhwc", d1, d2, what=f"DSB[{n1}|{n2}]", keep=k1 + k2)
-            return o3 if cv3 is not None else y
         if pre is not None:
             c2m, c1m, x0, y0 = pre
             (w2, b2), (w1, b1) = c2m.folded(), c1m.folded()

@@ -25,8 +25,8 @@ from ._lib import View, lib
 # The YDBL_* switches that change what a plan builds or launches (plan-builder fusions in ydbl.nn.modules / tasks,
 # routing in the C-ABI, read at build or at each launch).  tests/test_host_api.py checks this list against the
 # names the sources read.
-SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_DSB_PAIR", "YDBL_HG_UNFUSED",
-            "YDBL_HALO_SMALL", "YDBL_LSK_UNFUSED", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_SPLITK", "YDBL_SPLITK_BIG", "YDBL_NO_BNECK", "YDBL_NO_CV1_FUSE",
+SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_HG_UNFUSED",
+            "YDBL_HALO_SMALL", "YDBL_LSK_UNFUSED", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_SPLITK", "YDBL_NO_BNECK", "YDBL_NO_CV1_FUSE",
             "YDBL_NO_CV3_FUSE", "YDBL_NO_FUSE_PAD", "YDBL_NO_MERGE", "YDBL_NO_STEM2")
 
 
