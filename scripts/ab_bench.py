@@ -1,7 +1,7 @@
 """A/B of YDBL_* routing knobs on the bench workload in ONE process (same box, interleaved rounds), so box-to-box
 spread does not enter the comparison.  Each variant is a separate session (the session key holds the knobs).
 
-    python scripts/ab_bench.py "A:" "B:YDBL_NO_CV3_FUSE=1;YDBL_NO_MERGE=1" [--model n] [--batch 32] [--streams 2] [--rounds 5]
+    python scripts/ab_bench.py "A:" "B:YDBL_CV3_FUSE=1;YDBL_NO_MERGE=1" [--model n] [--batch 32] [--streams 2] [--rounds 5]
     python scripts/ab_bench.py "S2:" "S3:STREAMS=3" "S4:STREAMS=4"        (sub-batch graphs per variant)
 """
 import argparse

@@ -15,8 +15,20 @@ def _x(n, c, h=40, w=40, cs=None):
     return NS(n=n, c=c, h=h, w=w, cs=cs if cs is not None else c)
 
 
+def test_cv1_cv3_fusions_off_by_default(monkeypatch):
+    """Round 6: the leading / trailing 1x1 fusions are opt-in (YDBL_CV1_FUSE / YDBL_CV3_FUSE = 1): the separate
+    launches measured faster in the benched two-branch layout (profiles/r06/r06_fusion_switch_sweep.txt)."""
+    monkeypatch.delenv("YDBL_CV1_FUSE", raising=False)
+    monkeypatch.delenv("YDBL_CV3_FUSE", raising=False)
+    monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
+    m = M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=7)
+    plan = NS(dtype=torch.float16)
+    assert not m._cv1_fusable(plan, _x(16, 64)) and not m._cv3_fusable(plan, _x(16, 64))
+
+
 def test_cv1_fusable_dbl_n_shape(monkeypatch):
-    monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
+    monkeypatch.setenv("YDBL_CV1_FUSE", "1")
+    monkeypatch.setenv("YDBL_CV3_FUSE", "1")
     monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
     m = M.DSC3k(64, 64, 2, True, e=1.0, k1=3, k2=7)
     plan = NS(dtype=torch.float16)
@@ -28,12 +40,12 @@ def test_cv1_fusable_dbl_n_shape(monkeypatch):
     assert not m._cv1_fusable(plan, _x(16, 64))
     assert not m._cv3_fusable(plan, _x(16, 64))
     monkeypatch.delenv("YDBL_DS_LEAN")
-    monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")
+    monkeypatch.setenv("YDBL_CV1_FUSE", "0")
     assert not m._cv1_fusable(plan, _x(16, 64))
 
 
 def test_cv1_fusable_only_at_64_channels_and_k3(monkeypatch):
-    monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
+    monkeypatch.setenv("YDBL_CV1_FUSE", "1")
     monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
     plan = NS(dtype=torch.float16)
     assert not M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)._cv1_fusable(plan, _x(16, 128, 20, 20))
@@ -43,7 +55,7 @@ def test_cv1_fusable_only_at_64_channels_and_k3(monkeypatch):
 
 
 def test_cv3_fusable_small_map_rule_for_128_channels(monkeypatch):
-    monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
+    monkeypatch.setenv("YDBL_CV3_FUSE", "1")
     monkeypatch.delenv("YDBL_DS_LEAN", raising=False)
     plan = NS(dtype=torch.float16)
     m = M.DSC3k(128, 128, 2, True, e=1.0, k1=3, k2=7)

@@ -134,6 +134,34 @@ def test_conv_wsk_split_k(dtype, cin, cout, k, n, h, w, res):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+@pytest.mark.parametrize("cin,cout,n,h,w", [(384, 64, 16, 40, 40), (256, 32, 4, 80, 80), (64, 96, 17, 37, 45)])
+def test_conv3x3_halo_nblock(monkeypatch, dtype, cin, cout, n, h, w):
+    """The halo 3x3 kernel with two images per workgroup (YDBL_HALO_NB=2: every staged weight chunk feeds both
+    images' tiles; odd batches leave the last block's second image masked) vs F.conv2d fp32, and equal to the one-image
+    workgroups (the same per-output k order)."""
+    from ydbl import _lib
+    from ydbl.nn.modules import emit_dense
+
+    torch.manual_seed(cin + cout + n)
+    x = torch.randn(n, cin, h, w)
+    wt = torch.randn(cout, cin, 3, 3) / (cin * 9) ** 0.5
+    b = torch.randn(cout)
+    ref = F.silu(F.conv2d(x.to(dtype).float(), wt.to(dtype).float(), b, 1, 1))
+    outs = []
+    for nb in ("2", "1"):
+        monkeypatch.setenv("YDBL_HALO_NB", nb)
+        monkeypatch.setenv("YDBL_SPLITK", "0")
+        plan = _plan(dtype)
+        xv = _tv_from_nchw(plan, x, cs_extra=8, c_off=8)
+        yv = plan.alloc(n, h, w, cout + 8).cslice(4, cout)
+        emit_dense(plan, xv, yv, wt, b, 1, 1, 1, _lib.ACT_SILU)
+        _run(plan)
+        outs.append(yv.nchw().float().cpu())
+    torch.testing.assert_close(outs[0], ref, **_tol(dtype))
+    assert torch.equal(outs[0], outs[1]), (outs[0] - outs[1]).abs().max()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("cin,cout,n,h,w,res", [
     (128, 256, 4, 40, 40, "add"),  # DBL-s bs4 head 3x3: unsplittable (4 chunks), Cout 256 -> halo tile, 32-ch slices
     (64, 128, 3, 37, 41, None),    # ragged map, 2 chunks
@@ -1171,12 +1199,12 @@ def test_dsc3k_cv3_fused_bit_identical(c, n, shape, sliced, monkeypatch):
     o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=c).eval()
     x = torch.randn(*shape)
     outs, nsteps = [], []
-    monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")  # the leading-1x1 fusion has its own test (below)
+    monkeypatch.setenv("YDBL_CV1_FUSE", "0")  # the leading-1x1 fusion has its own test (below)
     for fuse in ("1", ""):
         if fuse:
-            monkeypatch.delenv("YDBL_NO_CV3_FUSE", raising=False)
+            monkeypatch.setenv("YDBL_CV3_FUSE", "1")
         else:
-            monkeypatch.setenv("YDBL_NO_CV3_FUSE", "1")
+            monkeypatch.setenv("YDBL_CV3_FUSE", "0")
         pm = M.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7)
         pm.load_state_dict(o.state_dict())
         plan = _plan(torch.float16)
@@ -1210,11 +1238,12 @@ def test_dsc3k_cv1_fused_bit_identical(n, shape, sliced, monkeypatch):
     o = trained_like_(om.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7), seed=7).eval()
     x = torch.randn(*shape)
     outs, nsteps = [], []
+    monkeypatch.setenv("YDBL_CV3_FUSE", "1")  # the leading 1x1 rides only in the trailing-GEMM layout (C3.emit)
     for fuse in ("1", ""):
         if fuse:
-            monkeypatch.delenv("YDBL_NO_CV1_FUSE", raising=False)
+            monkeypatch.setenv("YDBL_CV1_FUSE", "1")
         else:
-            monkeypatch.setenv("YDBL_NO_CV1_FUSE", "1")
+            monkeypatch.setenv("YDBL_CV1_FUSE", "0")
         pm = M.DSC3k(c, c, n, True, e=1.0, k1=3, k2=7)
         pm.load_state_dict(o.state_dict())
         plan = _plan(torch.float16)
@@ -1318,9 +1347,9 @@ def test_lsk_fused_bit_identical(c, shape, sliced, monkeypatch):
     outs = []
     for fused in ("1", ""):
         if fused:
-            monkeypatch.delenv("YDBL_LSK_UNFUSED", raising=False)
+            monkeypatch.setenv("YDBL_LSK_FUSE", "1")
         else:
-            monkeypatch.setenv("YDBL_LSK_UNFUSED", "1")
+            monkeypatch.setenv("YDBL_LSK_FUSE", "0")
         plan = _plan(torch.float16)
         xv = _tv_from_nchw(plan, x)
         out = plan.alloc(shape[0], shape[2], shape[3], c + 16).cslice(8, c) if sliced else None

@@ -25,7 +25,10 @@
 namespace ydbl {
 
 
-template <typename T, int S, int TH, int NTN, bool Q8>
+// NB > 1 (N-blocking): the workgroup takes the same tile of NB consecutive images, so every staged weight chunk feeds NB
+// times the MFMAs (the weights are most of a deep-K chunk's bytes: 384->64 @40^2, 8-row tile, 64 channels: 36.9 KB
+// of weights against 11.5 KB of halo per 32-channel chunk).
+template <typename T, int S, int TH, int NTN, bool Q8, int NB = 1>
 __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int tiles_x, int tiles_y,
                                                               int co_splits) {
   constexpr int TW = 16;
@@ -39,19 +42,19 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   constexpr int TMW = (TH + 3) / 4;  // 16-pixel tiles (= output rows) per wave
   using vec = typename Vec<T>::type;
   using opv = typename Op<T, Q8>::lds;  // 8-byte e4m3 groups in fp8 mode (same slot layout)
-  __shared__ opv s_x[XSLOTS];
+  __shared__ opv s_x[NB * XSLOTS];
   __shared__ opv s_w[WV];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int ntiles = p.N * tiles_y * tiles_x;
+  const int ntiles = (p.N + NB - 1) / NB * tiles_y * tiles_x;
   int bid = xcd_remap(blockIdx.x, ntiles * co_splits);
   const int cs = bid % co_splits;
   bid /= co_splits;
   const int tx = bid % tiles_x; bid /= tiles_x;
   const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
+  const int b0 = bid / tiles_y * NB;  // first image of the block
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const int co0 = cs * NTN * 16;
@@ -65,8 +68,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
   // source offsets are chunk-invariant and computed once.  (Lane maps that read whole 64-byte pieces per
   // lane quad cut the TCP accesses 3.2x and TD busy 1.7x but not the time: 384->64 @40^2 bs16 29.6 vs 30.2 us,
   // profiles/r05/r05_halo_lane_map_ab.txt.)
-  const T* xsrc[XIT];
-  bool xok[XIT];
+  const T* xsrc[NB][XIT];
+  bool xok[NB][XIT];
 #pragma unroll
   for (int it = 0; it < XIT; ++it) {
     const int slot = min(it * 256 + tid, XSLOTS - 1);
@@ -75,8 +78,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     const int px = blk * 16 * S + (r2 & 15) * S + r2 / 16;
     const int hy = px / IW, hx = px - hy * IW;
     const int iy = iy0 + hy, ix = ix0 + hx;
-    xok[it] = px < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
-    xsrc[it] = p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + gv * VEC;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int b = min(b0 + nb, p.N - 1);
+      xok[nb][it] = b0 + nb < p.N && px < NPIX && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+      xsrc[nb][it] = p.x + ((int64_t)(b * p.H + iy) * p.W + ix) * p.xcs + gv * VEC;
+    }
   }
   int64_t wsrc[WIT];  // element offsets into the weight matrix
   bool wok[WIT];
@@ -90,30 +97,35 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     wsrc[it] = (int64_t)min(co, p.Cout - 1) * p.KPAD + tap * p.Cin + gv * VEC;
   }
   // raw loads, zero selects at the LDS store (vload_clamped): the next chunk stays in flight during the MFMAs
-  vec xr[XIT];
+  vec xr[NB][XIT];
   opv wr[WIT];
   bool cok = true;
   auto load_chunk = [&](int c0) {
     cok = c0 < p.Cin;
 #pragma unroll
-    for (int it = 0; it < XIT; ++it) xr[it] = vload_clamped(xsrc[it] + c0, p.x, xok[it] && cok);
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int it = 0; it < XIT; ++it) xr[nb][it] = vload_clamped(xsrc[nb][it] + c0, p.x, xok[nb][it] && cok);
 #pragma unroll
     for (int it = 0; it < WIT; ++it) wr[it] = load_wop_raw<T, Q8>(p.w, wsrc[it] + c0, wok[it] && cok);
   };
   auto store_chunk = [&]() {
 #pragma unroll
-    for (int it = 0; it < XIT; ++it)
-      if (it * 256 + tid < XSLOTS) s_x[it * 256 + tid] = to_op<T, Q8>(vsel(xr[it], xok[it] && cok), p.qs);
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int it = 0; it < XIT; ++it)
+        if (it * 256 + tid < XSLOTS)
+          s_x[nb * XSLOTS + it * 256 + tid] = to_op<T, Q8>(vsel(xr[nb][it], xok[nb][it] && cok), p.qs);
 #pragma unroll
     for (int it = 0; it < WIT; ++it)
       if (it * 256 + tid < WV) s_w[it * 256 + tid] = vsel(wr[it], wok[it] && cok);
   };
 
-  f32x4 acc[NTN][TMW];
+  f32x4 acc[NTN][NB * TMW];  // [channel tile][image nb * TMW + row round j]
 #pragma unroll
   for (int i = 0; i < NTN; ++i)
 #pragma unroll
-    for (int j = 0; j < TMW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NB * TMW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // one LDS buffer, refilled between barriers; the next chunk is in registers during the MFMAs (two buffers and
   // one barrier per chunk measured even or slower: kbench bs16 384->64 @40^2 27.0 vs 26.7 us, 64->128 13.2 vs 15.7;
@@ -134,16 +146,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int ky = tap / 3, kx = tap % 3;
-      opv af[NTN], bf[TMW];
+      opv af[NTN], bf[NB * TMW];
 #pragma unroll
       for (int i = 0; i < NTN; ++i) af[i] = s_w[((i * 9 + tap) * 4 + g) * 16 + r16];
 #pragma unroll
-      for (int j = 0; j < TMW; ++j) {
-        const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
-        bf[j] = s_x[hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
-      }
+      for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-      for (int j = 0; j < TMW; ++j)
+        for (int j = 0; j < TMW; ++j) {
+          const int row = min(wave + 4 * j, TH - 1);  // clamped rows of a short last round are masked
+          bf[nb * TMW + j] = s_x[nb * XSLOTS + hslot<S>((row * S + ky) * IW + r16 * S + kx, g)];
+        }
+#pragma unroll
+      for (int j = 0; j < NB * TMW; ++j)
 #pragma unroll
         for (int i = 0; i < NTN; ++i) acc[i][j] = mfma_op<T, Q8>(af[i], bf[j], acc[i][j]);
     }
@@ -154,28 +168,30 @@ __global__ __launch_bounds__(256, 2) void conv3x3_halo_kernel(ConvArgs<T> p, int
     }
   }
 
-  int64_t pp[TMW];
-  bool pv[TMW];
+  int64_t pp[NB * TMW];
+  bool pv[NB * TMW];
 #pragma unroll
-  for (int j = 0; j < TMW; ++j) {
-    const int row = wave + 4 * j;
-    const int oy = oy0 + row, ox = ox0 + r16;
-    pv[j] = row < TH && oy < p.Ho && ox < p.Wo;
-    pp[j] = ((int64_t)b * p.Ho + oy) * p.Wo + ox;
-  }
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int j = 0; j < TMW; ++j) {
+      const int row = wave + 4 * j;
+      const int oy = oy0 + row, ox = ox0 + r16;
+      pv[nb * TMW + j] = b0 + nb < p.N && row < TH && oy < p.Ho && ox < p.Wo;
+      pp[nb * TMW + j] = ((int64_t)(b0 + nb) * p.Ho + oy) * p.Wo + ox;
+    }
   int co[NTN];
 #pragma unroll
   for (int i = 0; i < NTN; ++i) co[i] = co0 + i * 16 + 4 * g;
   if (p.ksplit > 1) {  // this split's partial tile (f32), summed + epilogue by splitk_epilogue_kernel (conv.hip)
     const int cs4 = (p.Cout + 3) & ~3;
 #pragma unroll
-    for (int j = 0; j < TMW; ++j)
+    for (int j = 0; j < NB * TMW; ++j)
 #pragma unroll
       for (int i = 0; i < NTN; ++i)
         if (pv[j] && co[i] < p.Cout) *reinterpret_cast<f32x4*>(p.ws + ((int64_t)z * p.P + pp[j]) * cs4 + co[i]) = acc[i][j];
     return;
   }
-  conv_epilogue<T, NTN, TMW, Q8>(p, acc, pp, pv, co, s_bias, co0);
+  conv_epilogue<T, NTN, NB * TMW, Q8>(p, acc, pp, pv, co, s_bias, co0);
 }
 
 template <typename T, bool Q8>
@@ -221,6 +237,20 @@ static void launch_halo(const ConvArgs<T>& a0, hipStream_t s) {
   // (512: the 64->128 @40^2 head convs of a bs16 graph, 480 workgroups, also gain: 14.3 -> 13.2 us, kbench;
   // 16-channel slices and 4-row tiles lose on every head shape: profiles/r05/r05_halo_tile_ab.txt)
   constexpr int64_t n2_below = 512;
+  // 8-row stride-1 tiles of two images per workgroup (N-blocking), 32-channel slices: half the weight staging per
+  // output; each launch takes longer, but with less CU time the two sub-batch branches overlap better -- DBL-n bs32
+  // +0.8 %, DBL-s bs64 / DBL-l 1280 bs8 +0.4 %, DBL-s bs8 even (profiles/r06/r06_fusion_switch_sweep.txt,
+  // r06_sweep2.txt; per launch in graph at bs16: 384->64 @40^2 28.3 -> 33.5 us, 192->64 17.6 -> 20.2).
+  // YDBL_HALO_NB=1 (read per launch; A/B switch): one image per workgroup.
+  if constexpr (S == 1 && TH == 8 && !Q8) {
+    const char* e = getenv("YDBL_HALO_NB");
+    if (!(e && *e == '1') && a.N >= 2) {
+      const int64_t nt2 = (int64_t)(a.N + 1) / 2 * tiles_y * tiles_x;
+      const int cs = (int)cdiv(a.Cout, 32);
+      conv3x3_halo_kernel<T, S, TH, 2, Q8, 2><<<(unsigned)(nt2 * cs), 256, 0, s>>>(a, tiles_x, tiles_y, cs);
+      return;
+    }
+  }
   if (a.Cout <= 32) {
     conv3x3_halo_kernel<T, S, TH, 2, Q8><<<(unsigned)ntiles, 256, 0, s>>>(a, tiles_x, tiles_y, 1);
   } else if (ntiles * cdiv(a.Cout, 64) < n2_below) {

@@ -102,13 +102,17 @@ __device__ unsigned long long g_st_stamps[8 * 16384];
 // One workgroup per tile.  (Measured and not kept: a persistent walk over 2-8 tiles per CU with the next
 // tile's window prefetched during the current tile's convs -- 140-166 vs 136 us at bs32: the kernel is VALU-
 // issue-bound on the first conv's SiLU, not latency-bound.)
-template <int C0, int TW, int TH, bool V4>
+// BOUND (a template flag, so the session's own unbound launch carries no binding code): x and scale from the input
+// binding (include/ydbl.h ydbl_input_bind), read once at the start.
+template <int C0, int TW, int TH, bool V4, bool BOUND>
 __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__ x, int H, int W, float scale,
                                                        const unsigned char* __restrict__ params,
                                                        DView<_Float16> y, int tiles_x, int tiles_y, int nblocks,
                                                        InputBind ib) {
-  x = bound_x(ib, x);
-  scale = bound_scale(ib, scale);
+  if constexpr (BOUND) {
+    x = *ib.x;
+    scale = *ib.amax > 1.0f + __FLT_EPSILON__ ? 1.0f / 255.0f : 1.0f;
+  }
   using Cfg = Stem2Cfg<C0, TW, TH>;
   const h8* w0f = reinterpret_cast<const h8*>(params);
   const h8* w1f = w0f + Cfg::W0F;
@@ -261,8 +265,7 @@ __global__ __launch_bounds__(256, 2) void stem2_kernel(const float* __restrict__
   }
 #endif
   const Tile tl = tile_of(blockIdx.x);
-  if (ib.x) load_window(tl, std::true_type{});
-  else load_window(tl, std::false_type{});
+  load_window(tl, std::integral_constant<bool, BOUND>{});
   {
     store_window();
     __syncthreads();
@@ -407,11 +410,17 @@ extern "C" int ydbl_conv_stem2(const ydbl_stem2_desc* d, void* stream) {
     return check_launch("ydbl_conv_stem2");
   };
   const bool v4 = d->w % 4 == 0 && (reinterpret_cast<uintptr_t>(d->x) & 15) == 0;
+  const bool bound = d->bind.x != nullptr;
 #define YDBL_STEM2_GO(C0_, TH_)                                                                                     \
-  return v4 ? go(stem2_kernel<C0_, 32, TH_, true>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)                           \
-            : go(stem2_kernel<C0_, 32, TH_, false>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)
-  if (c0 == 8) YDBL_STEM2_GO(8, 8);
-  if (c0 == 16) YDBL_STEM2_GO(16, 8);
+  {                                                                                                                  \
+    if (bound)                                                                                                       \
+      return v4 ? go(stem2_kernel<C0_, 32, TH_, true, true>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)                 \
+                : go(stem2_kernel<C0_, 32, TH_, false, true>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS);               \
+    return v4 ? go(stem2_kernel<C0_, 32, TH_, true, false>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS)                  \
+              : go(stem2_kernel<C0_, 32, TH_, false, false>, 32, TH_, Stem2Cfg<C0_, 32, TH_>::LDS);                \
+  }
+  if (c0 == 8) YDBL_STEM2_GO(8, 8)
+  if (c0 == 16) YDBL_STEM2_GO(16, 8)
 #undef YDBL_STEM2_GO
   return fail(YDBL_EINVAL, "stem2: c0 must be 8 or 16");
 }

@@ -712,8 +712,9 @@ class C3(PlanModule):
     def _cv1_fusable(self, plan, x) -> bool:
         """cv2 | cv1 (merged 1x1, x.c -> 2 c_) can lead the first DSBottleneck's k3 DSConv in one launch
         (dsc_lean.hip PRE, ydbl_dsconv_desc.g0): fp16, x.c == c_ == 64, SiLU 1x1s, that DSConv k3 stride 1 with
-        no depthwise bias, the lean kernel enabled."""
-        if (plan.dtype != torch.float16 or os.environ.get("YDBL_NO_CV1_FUSE") or os.environ.get("YDBL_DS_LEAN") == "0"
+        no depthwise bias, the lean kernel enabled -- and YDBL_CV1_FUSE=1: off by default since round 6 (the separate
+        1x1 measured faster in the two-branch layout: DBL-n bs32 +0.5 %, profiles/r06/r06_fusion_switch_sweep.txt)."""
+        if (plan.dtype != torch.float16 or os.environ.get("YDBL_CV1_FUSE") != "1" or os.environ.get("YDBL_DS_LEAN") == "0"
                 or not len(self.m) or not isinstance(self.m[0], DSBottleneck)):
             return False
         c_ = self.cv1.conv.out_channels
@@ -727,10 +728,11 @@ class C3(PlanModule):
     def _cv3_fusable(self, plan, x) -> bool:
         """cv3 can run as the trailing GEMM of the last bottleneck's k7 DSConv (dsc_lean.hip, ydbl_dsconv_desc.g2):
         fp16, m = DSBottlenecks ending in a k7 stride-1 DSConv with c_ in {64, 128} in and out, cv3 a 1x1 SiLU
-        Conv 2c_ -> c_ (DSC3k with e = 1, U/nn/modules/block.py:1447-1503)."""
+        Conv 2c_ -> c_ (DSC3k with e = 1, U/nn/modules/block.py:1447-1503) -- and YDBL_CV3_FUSE=1: off by default since
+        round 6 (DBL-n bs32 +0.6 % with the separate cv3, profiles/r06/r06_fusion_switch_sweep.txt)."""
         # the trailing GEMM runs only in the lean kernel (dsc_lean.hip): with it switched off the chunked kernel
         # would refuse the g2 descriptor, so the rule must agree with _cv1_fusable's
-        if (plan.dtype != torch.float16 or os.environ.get("YDBL_NO_CV3_FUSE") or os.environ.get("YDBL_DS_LEAN") == "0"
+        if (plan.dtype != torch.float16 or os.environ.get("YDBL_CV3_FUSE") != "1" or os.environ.get("YDBL_DS_LEAN") == "0"
                 or not len(self.m)):
             return False
         last, c_ = self.m[-1], self.cv1.conv.out_channels
@@ -1117,7 +1119,11 @@ class LSKblock(PlanModule):
         half = self.conv1.out_channels
         a1, a2 = emit_dw_pair(plan, self.conv0, self.conv_spatial, x, what="LSK.dw5+dw7d3")
         y = out if out is not None else plan.alloc(x.n, x.h, x.w, x.c)
-        if (plan.dtype == torch.float16 and x.c in (256, 512) and not os.environ.get("YDBL_LSK_UNFUSED")
+        # fused at dim 256 (DBL-n); at 512 (DBL-s) the five launches measured faster in the two-branch layout:
+        # DBL-s bs8 per rank +1.6 %, bs64 +0.4 %; DBL-n bs32 fused +1.1 % (profiles/r06/r06_fusion_switch_sweep.txt,
+        # r06_sweep2.txt).  YDBL_LSK_FUSE=1 / 0 forces either.
+        fuse = os.environ.get("YDBL_LSK_FUSE")
+        if (plan.dtype == torch.float16 and x.c in (256, 512) and (fuse == "1" or (fuse is None and x.c == 256))
                 and vec_aligned(x) and vec_aligned(y) and y.base is not x.base):
             # conv1 | conv2 + stats, then gate + conv + x * in two launches (csrc/lsk.hip)
             attn = plan.alloc(x.n, x.h, x.w, 2 * half)
