@@ -26,6 +26,17 @@ def test_cv1_cv3_fusions_off_by_default(monkeypatch):
     assert not m._cv1_fusable(plan, _x(16, 64)) and not m._cv3_fusable(plan, _x(16, 64))
 
 
+def test_dwpw_fused_default_at_64_outputs(monkeypatch):
+    """The Detect DWConv -> Conv1x1 pairs run as one launch at 64 pointwise outputs (DBL-n) and as two at 128+
+    (DBL-s / DBL-l), unless YDBL_DWPW forces either (profiles/r06/r06_detect_switch_sweep.txt)."""
+    monkeypatch.delenv("YDBL_DWPW", raising=False)
+    assert M.dwpw_fuse(64) and not M.dwpw_fuse(128)
+    monkeypatch.setenv("YDBL_DWPW", "1")
+    assert M.dwpw_fuse(128)
+    monkeypatch.setenv("YDBL_DWPW", "0")
+    assert not M.dwpw_fuse(64)
+
+
 def test_cv1_fusable_dbl_n_shape(monkeypatch):
     monkeypatch.setenv("YDBL_CV1_FUSE", "1")
     monkeypatch.setenv("YDBL_CV3_FUSE", "1")

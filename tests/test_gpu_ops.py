@@ -445,9 +445,11 @@ def test_conv_fp8(cin, cout, k, n, h, w, res, s):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
 @pytest.mark.parametrize("c,c2,shape", [(64, 64, (2, 64, 40, 40)), (128, 64, (2, 128, 20, 21)), (64, 80, (1, 64, 13, 17))])
-def test_detect_dw_pw_fused(dtype, c, c2, shape):
+def test_detect_dw_pw_fused(dtype, c, c2, shape, monkeypatch):
     """Detect cv3 pair DWConv(c,c,3) -> Conv(c,c2,1) (head.py:93-101) as one fused depthwise->pointwise
-    launch: dw bias + SiLU applied in LDS before the pointwise MFMA."""
+    launch: dw bias + SiLU applied in LDS before the pointwise MFMA (forced with YDBL_DWPW=1: by default only
+    c2 <= 64 takes it, modules.dwpw_fuse)."""
+    monkeypatch.setenv("YDBL_DWPW", "1")
     from oracle import model as om
     from ydbl.nn import modules as M
 

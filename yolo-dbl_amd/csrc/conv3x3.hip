@@ -243,6 +243,7 @@ static void launch_halo(const ConvArgs<T>& a0, hipStream_t s) {
   // r06_sweep2.txt; per launch in graph at bs16: 384->64 @40^2 28.3 -> 33.5 us, 192->64 17.6 -> 20.2).
   // YDBL_HALO_NB=1 (read per launch; A/B switch): one image per workgroup.
   if constexpr (S == 1 && TH == 8 && !Q8) {
+    // (four images per workgroup, or two in 64-channel slices: DBL-n bs32 -3.1 / -2.3 %, r06_sweep3_cumask.txt)
     const char* e = getenv("YDBL_HALO_NB");
     if (!(e && *e == '1') && a.N >= 2) {
       const int64_t nt2 = (int64_t)(a.N + 1) / 2 * tiles_y * tiles_x;

@@ -237,13 +237,15 @@ def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = N
     when the shapes allow (the depthwise output stays in LDS), else two.  With tail_conv (the class conv
     cv3[i][2], 1x1 c2 -> nc, bias) the launch also writes tail_out when c2 == 64 and nc <= 4; returns
     (y, tail_done)."""
-    if fused_dsconv_ok(dwc.conv, x, plan.dtype) and pwc.conv.kernel_size == (1, 1) and pwc.conv.stride == (1, 1):
+    if (fused_dsconv_ok(dwc.conv, x, plan.dtype) and pwc.conv.kernel_size == (1, 1) and pwc.conv.stride == (1, 1)
+            and dwpw_fuse(pwc.conv.out_channels)):
         wd, bdw = dwc.folded()
         wp, bp = pwc.folded()
         if bdw is None:
             bdw = torch.zeros(x.c)
         tail = None
-        if (tail_conv is not None and wp.shape[0] == 64 and tail_conv.kernel_size == (1, 1) and tail_conv.groups == 1
+        if (tail_conv is not None and not os.environ.get("YDBL_NO_CLS_TAIL") and wp.shape[0] == 64
+                and tail_conv.kernel_size == (1, 1) and tail_conv.groups == 1
                 and tail_conv.in_channels == 64 and 1 <= tail_conv.out_channels <= 4 and tail_conv.bias is not None):
             nc = tail_conv.out_channels
             tail = (tail_conv.weight.detach().float().reshape(nc, 64), tail_conv.bias.detach().float(), tail_out)
@@ -251,6 +253,14 @@ def emit_dw_pw(plan: Plan, dwc: "DWConv", pwc: "Conv", x: TV, out: TV | None = N
                         _act_code(pwc.act), what=what, w_dw=wd, b_dw=bdw, dw_act=_act_code(dwc.act), tail=tail)
         return y, tail is not None
     return pwc.emit(plan, dwc.emit(plan, x), out), False
+
+
+def dwpw_fuse(c2: int) -> bool:
+    """Whether the Detect DWConv -> Conv1x1 pair runs as one launch: at 64 pointwise outputs (DBL-n) the fused pair
+    is faster (separate: DBL-n bs32 -1.8 %), at 128 and more (DBL-s / DBL-l) the two launches are (DBL-s bs8 +1.1 %,
+    bs64 +2.0 %, DBL-l 1280 bs8 +1.9 %: profiles/r06/r06_detect_switch_sweep.txt).  YDBL_DWPW=1 / 0 forces either."""
+    e = os.environ.get("YDBL_DWPW")
+    return e == "1" or (e is None and c2 <= 64)
 
 
 def stem_ok(m, ch: int) -> bool:
@@ -569,7 +579,8 @@ def emit_conv3x3_pair(plan, a: "Conv", b: "Conv", x: TV, out: TV | None = None) 
     cv2[i][0:2] at 64 channels, head.py:86-90), else the two convs."""
     ca, cb = a.conv, b.conv
     c, cm = cb.out_channels, ca.out_channels
-    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and (c, cm) == (64, 64)
+    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and not os.environ.get("YDBL_NO_PAIR3")
+          and (c, cm) == (64, 64)
           and x.c == c == ca.in_channels and cb.in_channels == cm
           and all(m.kernel_size == (3, 3) and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1)
                   and m.groups == 1 for m in (ca, cb))
@@ -593,7 +604,8 @@ def emit_detect_box(plan, seq, x: TV, out: TV) -> bool:
     emitted) unless fp16 with c_in 64 or 128 (DBL-n P3 / P4)."""
     a, b, c = seq[0], seq[1], seq[2]
     ca, cb = a.conv, b.conv
-    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and x.c in (64, 128)
+    ok = (plan.dtype == torch.float16 and not os.environ.get("YDBL_NO_BNECK") and not os.environ.get("YDBL_NO_BOX3")
+          and x.c in (64, 128)
           and ca.in_channels == x.c and ca.out_channels == cb.in_channels == cb.out_channels == 64
           and all(m.kernel_size == (3, 3) and m.stride == (1, 1) and m.padding == (1, 1) and m.dilation == (1, 1)
                   and m.groups == 1 for m in (ca, cb))
