@@ -3,6 +3,8 @@ spread does not enter the comparison.  Each variant is a separate session (the s
 
     python scripts/ab_bench.py "A:" "B:YDBL_CV3_FUSE=1;YDBL_NO_MERGE=1" [--model n] [--batch 32] [--streams 2] [--rounds 5]
     python scripts/ab_bench.py "S2:" "S3:STREAMS=3" "S4:STREAMS=4"        (sub-batch graphs per variant)
+A variant listed twice under two names ("A:" ... "A2:") is two sessions with the same routing: their spread is the
+session-to-session bias (buffer placement), about 0.5 % on DBL-n bs32 (profiles/r06/r06_defaults_ab.txt).
 """
 import argparse
 import os
@@ -62,6 +64,8 @@ def main():
     res = {k: [] for k in sess}
     for _ in range(a.rounds):
         for name, (s, _) in sess.items():
+            for _ in range(3):  # untimed: the previous variant's buffers leave the caches first
+                s()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.steps):

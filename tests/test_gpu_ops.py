@@ -292,9 +292,12 @@ def test_conv_tile(dtype, cin, cout, s, h, w, res):
     (16, 384, 64, 40, 40, None),      # bs16 sub-batch head conv: < 400 workgroups -> 32-channel slices
     (16, 192, 48, 40, 40, "add"),     # 32-channel slices, partial second slice, residual
 ])
-def test_conv3x3_halo(dtype, n, cin, cout, h, w, res):
+def test_conv3x3_halo(dtype, n, cin, cout, h, w, res, monkeypatch):
     """3x3 stride-1 convs with Cin >= 64 on >= 25600 output pixels: the halo-tiled kernel (8/16-row tiles,
-    64- or 32-channel slices)."""
+    64- or 32-channel slices; YDBL_HALO_T16=1 and YDBL_HALO_NB=1 so the 16-row and one-image forms stay covered --
+    the default N-blocked form has test_conv3x3_halo_nblock)."""
+    monkeypatch.setenv("YDBL_HALO_T16", "1")
+    monkeypatch.setenv("YDBL_HALO_NB", "1")
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense
 
@@ -361,8 +364,10 @@ def test_conv3x3_halo_s2(dtype, n, cin, cout, h, w, res):
     (17, 64, 64, 40, 40, None),       # 64->64 is routed here for 25600 < N*H*W <= 65536
     (30, 64, 64, 37, 29, "add"),
 ])
-def test_conv3x3_vw(n, cin, cout, h, w, res):
-    """fp16 3x3 stride-1 128->64 and mid-size 64->64 convs: the VGPR-weight kernel (conv3x3.hip)."""
+def test_conv3x3_vw(n, cin, cout, h, w, res, monkeypatch):
+    """fp16 3x3 stride-1 128->64 and mid-size 64->64 convs: the VGPR-weight kernel (conv3x3.hip; YDBL_VW=1, off by
+    default since round 6)."""
+    monkeypatch.setenv("YDBL_VW", "1")
     from ydbl import _lib
     from ydbl.nn.modules import emit_dense
 

@@ -615,7 +615,12 @@ template <typename T>
 static void wsk_tiles(const ConvArgs<T>& a, int& bm, int& bn) {
   auto blocks = [&](int m, int n) { return cdiv(a.P, m) * cdiv(a.Cout, n); };
   const int64_t want = 768;
-  if (a.Cout <= 128 && blocks(32, a.Cout <= 64 ? 64 : 128) < 256) { bm = a.Cout <= 64 ? 16 : 32; bn = 64; return; }
+  const char* eh = getenv("YDBL_WSK_HALF");  // A/B switch (read per launch): 0 = no half-height tiles
+  if (a.Cout <= 128 && blocks(32, a.Cout <= 64 ? 64 : 128) < 256 && !(eh && *eh == '0')) {
+    bm = a.Cout <= 64 ? 16 : 32;
+    bn = 64;
+    return;
+  }
   if (a.Cout <= 32) { bm = blocks(128, 32) >= want ? 128 : 64; bn = 32; return; }
   if (a.Cout <= 64) { bm = blocks(64, 64) >= want ? 64 : 32; bn = 64; return; }
   bm = 32;

@@ -310,7 +310,11 @@ bool try_conv3x3_halo(const ConvArgs<T>& a, int kh, hipStream_t s) {
   (void)tiles8;
   // Cout <= 32 (one 32-channel slice: the weights are as many bytes per chunk as the halo): 16-row tiles from
   // 256 of them (DBL-n's 256->32 @80^2 at bs16, 400 tiles: 34.6 -> 31.8 us in graph, scripts/kbench.py)
-  if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256)) launch_halo<T, Q8, 1, 16>(a, s);
+  // 16-row tiles only with YDBL_HALO_T16=1 (read per launch): the N-blocked 8-row tiles measured even to +0.7 % against
+  // them in the two-branch layout (profiles/r06/r06_conv_route_sweep.txt)
+  const char* e16 = getenv("YDBL_HALO_T16");
+  if (a.Ho % 16 == 0 && (a.Cout > 32 ? tiles16 >= 512 : tiles16 >= 256) && e16 && *e16 == '1')
+    launch_halo<T, Q8, 1, 16>(a, s);
   else launch_halo<T, Q8, 1, 8>(a, s);
   return true;
 }
@@ -443,6 +447,11 @@ static void launch_vw(const ConvArgs<_Float16>& a, int cs, hipStream_t s) {
 // 64->32 @80^2 22.5 -> 39.5, 64->128 @40^2 26.0 -> 29.4, 64->64 @20^2 8.9 -> 10.0 us).
 bool try_conv3x3_vw(const ConvArgs<_Float16>& a, int kh, hipStream_t s) {
   if (kh != 3 || a.KW != 3 || a.PAD != 1 || a.DIL != 1 || a.S != 1) return false;
+  // Round 6: off by default -- the N-blocked halo tile takes these shapes (DBL-n bs32 +0.4 %, DBL-s bs8 +0.7 %, bs64
+  // +1.5 %, profiles/r06/r06_conv_route_sweep.txt: less CU time per image in the two-branch layout, though each launch
+  // is longer).  YDBL_VW=1 (read per launch) routes them here.
+  const char* e = getenv("YDBL_VW");
+  if (!(e && *e == '1')) return false;
   if (a.xcs % 8 || a.H != a.Ho || a.W != a.Wo || (int64_t)a.N * a.Ho * a.Wo >= (1LL << 31)) return false;
   if (a.Cin == 128 && a.Cout == 64) return launch_vw<128, 1, 4, 2>(a, 1, s), true;
   constexpr int64_t vw_min = 25601;

@@ -26,7 +26,7 @@ from ._lib import View, lib
 # routing in the C-ABI, read at build or at each launch).  tests/test_host_api.py checks this list against the
 # names the sources read.
 SWITCHES = ("YDBL_DS2_OFF", "YDBL_DS_LEAN", "YDBL_HG_UNFUSED",
-            "YDBL_HALO_NB", "YDBL_HALO_SMALL", "YDBL_LSK_FUSE", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_SPLITK", "YDBL_NO_BNECK", "YDBL_NO_BOX3", "YDBL_NO_CLS_TAIL", "YDBL_DWPW", "YDBL_NO_PAIR3", "YDBL_CV1_FUSE",
+            "YDBL_HALO_NB", "YDBL_HALO_SMALL", "YDBL_HALO_T16", "YDBL_VW", "YDBL_WSK_HALF", "YDBL_LSK_FUSE", "YDBL_NMS_FAST", "YDBL_NMS_GROUPS", "YDBL_SPLITK", "YDBL_NO_BNECK", "YDBL_NO_BOX3", "YDBL_NO_CLS_TAIL", "YDBL_DWPW", "YDBL_NO_PAIR3", "YDBL_CV1_FUSE",
             "YDBL_CV3_FUSE", "YDBL_NO_FUSE_PAD", "YDBL_NO_MERGE", "YDBL_NO_STEM2")
 
 
