@@ -2,6 +2,7 @@
 
 from types import SimpleNamespace as NS
 
+import pytest
 import torch
 
 from ydbl.quant import candidate_macs, select_by_mac_budget
@@ -40,12 +41,14 @@ def test_selected_fraction_with_a_stride2_candidate():
     assert chosen == [] and frac == 0.0
 
 
-def test_candidate_keys_stable_across_layouts():
+@pytest.mark.parametrize("cv3_fuse", ["", "1"])
+def test_candidate_keys_stable_across_layouts(cv3_fuse, monkeypatch):
     """ydbl.quant.candidate_keys names a model's fp8 candidates the same way at every batch / sub-batch size, so one
     committed calibration (tests/golden/fp8_calib_*.json) means one layer set for every layout the model runs."""
     from ydbl import YOLO
     from ydbl.quant import candidate_keys
 
+    monkeypatch.setenv("YDBL_CV3_FUSE", cv3_fuse or "0")
     m = YOLO("yolov13s_DBL.yaml", nc=3).model
     keys = {}
     for b in (1, 4, 16, 32):
@@ -55,9 +58,12 @@ def test_candidate_keys_stable_across_layouts():
         assert all(int(key[1:].split(".")[0]) >= 0 for key in k)  # every candidate knows its layer
         keys[b] = k
     assert keys[16] == keys[32]
-    # small maps fold DSC3k's 128-channel cv3 into the lean DSConv launch (no longer a candidate): the others keep
-    # their names
-    assert set(keys[1]) == set(keys[4]) < set(keys[32])
+    if cv3_fuse:
+        # small maps fold DSC3k's 128-channel cv3 into the lean DSConv launch (no longer a candidate): the others
+        # keep their names
+        assert set(keys[1]) == set(keys[4]) < set(keys[32])
+    else:  # the default since round 6: cv3 is its own launch (a candidate) at every size
+        assert set(keys[1]) == set(keys[4]) == set(keys[32])
 
 
 def test_calibration_roundtrip_and_shares(tmp_path):
